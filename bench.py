@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X ray-trace hot path (BASELINE.json metric).
+
+  python bench.py [--gpus N --steps K --warmup W] [--config C3]
+
+One step = one render of the whole image of the workload (every primary,
+shadow, refraction and reflection ray of the reference's TraceRay count,
+SURVEY.md §8a).  Workload (N=1 and the default): config C3 of BASELINE.json,
+4096x4096, 1000 spheres + 1000 triangles, reflection/refraction depth 4,
+seeded synthetic scene (simple-raytracer_amd/rtamd/scenes.py).
+
+Multi-GPU (torchrun, one process per GPU): the image's rows are split into
+contiguous strips, one per rank (strong scaling: the image is fixed); each
+rank renders its strip into HBM and the strips are gathered to rank 0 over
+RCCL (torch.distributed "nccl").  Timed region: barrier + synchronize on both
+sides, K steps, max over ranks.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "simple-raytracer_amd"))
+
+PEAK_FP32_TFLOPS = 157.3        # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBPS = 8000.0          # HBM3E spec
+FLOP_SPHERE, FLOP_TRI = 20, 42  # algorithmic FLOPs per ray-primitive test
+
+WORKLOADS = {
+    "C2": "C2: 1024x1024, 100 spheres, 2 point lights, no reflection/refraction",
+    "C3": "C3: 4096x4096, 1000 spheres + 1000 triangles, reflection+refraction depth 4, 2 point lights",
+    "C4": "C4: 8192x8192, 10k textured triangles, 1 directional + 1 point light (hard shadows)",
+    "C5": "C5: 16384x16384, 100k spheres, reflection+refraction depth 8",
+}
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--cpu-sample", type=int, default=128,
+                    help="cpu_baseline: the reference renders the same scene at NxN")
+    ap.add_argument("--option", action="append", default=[],
+                    help="kernel option key=value (rt_scene_set_option)")
+    ap.add_argument("--out-json", default=None)
+    return ap.parse_args()
+
+
+def scene_dir() -> str:
+    d = os.path.join(os.environ.get("TMPDIR", tempfile.gettempdir()), "rtamd_bench_scenes")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
+    """The REAL reference (oracle/_ref/SimpleRayTracer, compiled from the
+    reference's own sources by oracle/Makefile) timed on this host's cores on a
+    bounded sample: the same seeded scene at sample x sample pixels (the whole
+    field of view, 1/(W*H/sample^2) of the pixels).  Rays of the sample are
+    counted by the GPU path on the same scene file (counts are parity-tested
+    equal to the reference's TraceRay calls)."""
+    from rtamd import scenes as gen
+    ref = os.path.join(ROOT, "oracle", "_ref", "SimpleRayTracer")
+    d = tempfile.mkdtemp(prefix="rtamd_cpu_")
+    path = gen.write_scene(d, config, w=sample, h=sample, tag=f"{config}_{sample}")
+    rays = gpu_rays_fn(path)
+    if os.path.exists(ref):
+        t0 = time.perf_counter()
+        subprocess.run([ref, os.path.basename(path)], cwd=d, check=True, stdout=subprocess.DEVNULL)
+        dt = time.perf_counter() - t0
+        return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
+                "sample": f"{config} scene at {sample}x{sample} (full field of view), {rays} rays, "
+                          f"{dt:.1f} s, single-threaded reference binary"}
+    # fall back to this repo's C restatement on all cores (a port, not the reference)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleScene
+    o = OracleScene(path)
+    t0 = time.perf_counter()
+    _, cnt = o.render(threads=0)
+    dt = time.perf_counter() - t0
+    r = sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection"))
+    return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": os.cpu_count(), "kind": "port",
+            "sample": f"{config} scene at {sample}x{sample}, oracle restatement, {dt:.1f} s"}
+
+
+def load_pmc_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(config, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main() -> None:
+    args = parse_args()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import rtamd
+    from rtamd import scenes as gen
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit("bench.py --gpus N>1 must be launched with torchrun (one process per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = gen.CONFIGS[args.config]
+    sd = os.path.join(scene_dir(), f"rank{rank}")
+    path = gen.write_scene(sd, args.config)
+    hs = rtamd.HostScene(path, cwd=sd)
+    hs.set_depth(cfg["depth"])
+    W, H = hs.width, hs.height
+    cam = hs.camera()
+    gs = rtamd.GpuScene(hs, device=local)
+    for kv in args.option:
+        k, v = kv.split("=")
+        gs.set_option(k, int(v))
+
+    # strong scaling: contiguous row strips, equal counts for the gather
+    rows_per = (H + world - 1) // world
+    y0 = min(H, rank * rows_per)
+    y1 = min(H, y0 + rows_per)
+    strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device="cuda")
+    gather_list = None
+    if world > 1 and rank == 0:
+        gather_list = [torch.empty_like(strip) for _ in range(world)]
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        if y1 > y0:
+            gs.render_rows_async(cam, W, H, y0, y1, strip.data_ptr(), stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.gather(strip, gather_list, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    st = gs.last_stats()
+    my_rays = st.rays()
+
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
+
+    t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms))], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, rays_total, kmax = float(tmax[0]), float(tsum[1]), float(tmax[2])
+    else:
+        rays_total, kmax = float(my_rays), float(np.mean(kernel_ms))
+
+    if rank == 0:
+        value = rays_total * args.steps / elapsed / 1e6
+        ns, nt = cfg["spheres"], cfg["tris"]
+        flop_per_ray = FLOP_SPHERE * ns + FLOP_TRI * nt
+        # dominant kernel = render_kernel; per launch on rank 0 (its strip)
+        k_s = float(np.mean(kernel_ms)) / 1e3
+        flops = my_rays * flop_per_ray
+        achieved = flops / k_s / 1e12
+        px = (y1 - y0) * W
+        scene_bytes = 80 * nt + 16 * ns + 52 * (ns + nt)
+        alg_bytes = 12 * px + scene_bytes
+        traffic = load_pmc_traffic(args.config)
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            def gpu_rays(p):
+                _, s = rtamd.render_scene(p, cwd=os.path.dirname(p), depth=cfg["depth"], device=local)
+                return s.rays()
+            try:
+                cpu = cpu_baseline(args.config, args.cpu_sample, gpu_rays)
+            except Exception as e:  # never lose the GPU line to the CPU leg
+                cpu = {"error": repr(e)}
+        line = {
+            "metric": "Mrays/s (primary+secondary)",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded scene generator, rtamd/scenes.py)",
+            "config": {"workload": WORKLOADS[args.config], "imsize": [W, H], "spheres": ns,
+                       "triangles": nt, "depth": cfg["depth"], "lights": 2,
+                       "rays_per_step": int(rays_total), "parallelism": f"row-strips x{world}"
+                       + (" + RCCL gather" if world > 1 else "")},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": traffic, "kernel": "render_kernel",
+                         "kernel_ms": round(float(np.mean(kernel_ms)), 3),
+                         "flop_per_ray": flop_per_ray, "rays_per_launch": my_rays,
+                         "hbm": {"alg_bytes_per_launch": alg_bytes,
+                                 "achieved_GBps": round(alg_bytes / k_s / 1e9, 3),
+                                 "peak_GBps": PEAK_HBM_GBPS,
+                                 "frac": round(alg_bytes / k_s / 1e9 / PEAK_HBM_GBPS, 7)}},
+            "cpu_baseline": cpu,
+            "ray_counts": {k: int(getattr(st, k)) for k in ("primary", "shadow", "refraction",
+                                                             "reflection", "skip_trans", "ub_back")},
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out_json:
+            with open(args.out_json, "w") as f:
+                f.write(s + "\n")
+    gs.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X (gfx950) ray-trace layer.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * has no plugin API; its seam is the single call
+ *
+ *     Mat3D create_view_window_and_ray_trace(eye, viewdir.norm(), updir.norm(),
+ *                                            fov_h, height, width, bkg);
+ *         -- /root/reference/main.cpp:607 (definition :670-767)
+ *
+ * plus the implicit inputs it reads from the global `Globals environment`
+ * (main.cpp:58, type src/definitions.h:304-311): spheres, faces, lights,
+ * materials, textures, "epsilon", "recursion_depth", "bkg_refraction_index".
+ * Under it run TraceRay (main.cpp:1215-1407) and ShadeRay (main.cpp:783-1207).
+ *
+ * Here that seam is split into: an explicit, POD scene description
+ * (rt_scene_desc: what `environment` held), a per-image camera (rt_camera:
+ * main.cpp:677-710, computed on the host by rt_host.h's rth_camera) and a
+ * row-range render (rt_render_rows: the pixel loop main.cpp:718-764 and
+ * everything below it) returning pre-quantisation float RGB.  Quantisation
+ * to the reference's size_t pixels (main.cpp:760-762) and the P3 writer
+ * (main.cpp:613-650) live in rt_host.h.
+ *
+ * Conventions: plain C, no exceptions cross the ABI, every function returns
+ * RT_OK (0) or a negative RT_E_* code (rt_strerror gives the text).  The
+ * caller owns every buffer it passes; the library keeps device copies inside
+ * rt_scene and never retains caller pointers after a call returns.
+ * rt_scene objects are per device; distinct scenes may be used from
+ * different host threads concurrently.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_E_INVALID (-1)     /* bad argument / malformed description */
+#define RT_E_NODEVICE (-2)    /* no such HIP device */
+#define RT_E_HIP (-3)         /* a HIP runtime call failed */
+#define RT_E_NOMEM (-4)       /* device allocation failed */
+#define RT_E_UNSUPPORTED (-5) /* e.g. recursion depth above the compiled maximum */
+
+/* Material (src/definitions.h:249-253, parsed at main.cpp:272-308). */
+typedef struct {
+    float diffuse[3];
+    float specular[3];
+    float ka, kd, ks, n;
+    float opacity;       /* already clamped to [0,1] by the parser (main.cpp:294) */
+    float eta;           /* refraction index */
+} rt_material;
+
+/* 'sphere' (main.cpp:328-377). texture = index into textures, or -1. */
+typedef struct {
+    float center[3];
+    float radius;
+    rt_material mat;
+    int texture;
+} rt_sphere_desc;
+
+/* 'f' (main.cpp:470-552).  v/vn/vt are the resolved vertex data (missing
+ * indices resolve to zero, like the reference's std::map::operator[]).
+ * smooth = the reference's smooth_shading flag (decided by the LAST vertex
+ * token's format). */
+typedef struct {
+    float v[3][3];
+    float vn[3][3];
+    float vt[3][2];
+    int smooth;
+    rt_material mat;
+    int texture;
+} rt_face_desc;
+
+/* 'light x y z w r g b' (main.cpp:378-411): w == 0 -> directional (xyz is the
+ * direction), else point (xyz is the position). */
+typedef struct {
+    float xyz[3];
+    float w;
+    float color[3];
+} rt_light_desc;
+
+/* P3 texture (src/utility.h:59-139): rgb is [height][width][3] bytes. */
+typedef struct {
+    int width, height;
+    const unsigned char *rgb;
+} rt_texture_desc;
+
+/* Everything the reference kept in `environment` for the hot path.  Objects
+ * are given per type in FILE order; the renderer visits all faces before all
+ * spheres, as the reference's std::map<string,...> iteration does
+ * (main.cpp:1218). */
+typedef struct {
+    int n_spheres;
+    const rt_sphere_desc *spheres;
+    int n_faces;
+    const rt_face_desc *faces;
+    int n_lights;
+    const rt_light_desc *lights;
+    int n_textures;
+    const rt_texture_desc *textures;
+    float bkg[3];        /* bkgcolor r g b */
+    float eta_bkg;       /* bkgcolor 4th arg; 0 when absent (main.cpp:751 default-insert) */
+    float epsilon;       /* 1e-3 (main.cpp:101) */
+    int depth;           /* recursion depth, 4 in the reference (main.cpp:100) */
+} rt_scene_desc;
+
+/* Per-image constants of main.cpp:677-710: pixel (i, j) looks along
+ * ((ul + dh*j) + dv*i) - eye. */
+typedef struct {
+    float eye[3];
+    float ul[3];
+    float dh[3];
+    float dv[3];
+} rt_camera;
+
+/* Ray counters.  One ray = one TraceRay call of the reference. */
+typedef struct {
+    unsigned long long primary;
+    unsigned long long shadow;
+    unsigned long long refraction;
+    unsigned long long reflection;
+    unsigned long long skip_trans;   /* 'goto SKIP_TRANS' taken (main.cpp:1001) */
+    unsigned long long ub_back;      /* back() on an empty medium stack (main.cpp:1028, UB in the reference) */
+    double kernel_ms;                /* device time of the render kernel(s) */
+} rt_stats;
+
+typedef struct rt_scene rt_scene;
+
+int rt_device_count(void);
+
+/* Upload a scene to HIP device `device`. */
+int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out);
+int rt_scene_destroy(rt_scene *scene);
+
+/* Render image rows [y0, y1) of a W x H image into out_rgb, which holds
+ * (y1 - y0) * W * 3 floats (row-major, RGB) and may be host or device
+ * memory.  Synchronous.  stats may be NULL. */
+int rt_render_rows(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
+                   rt_stats *stats);
+
+/* Same, asynchronous on `hip_stream` (a hipStream_t, NULL = the scene's own
+ * stream); out_rgb must be device memory.  rt_scene_last_stats() waits for
+ * the render and returns its counters. */
+int rt_render_rows_async(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
+                         void *hip_stream);
+int rt_scene_last_stats(rt_scene *scene, rt_stats *stats);
+
+/* Kernel selection / tuning knobs (0 = automatic). */
+int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
+
+const char *rt_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

@@ -1,0 +1,117 @@
+// rt_cli.cpp -- drop-in replacement for the reference executable
+// (`SimpleRayTracer <scene.txt>`, main.cpp:60-657): parses the scene, renders
+// it on MI355X through the C ABI of rt_hip.h and writes <scene>.ppm in the
+// reference's P3 format.  Messages and exit behaviour follow main():
+//   no argument          -> stdout message, exit 0           (main.cpp:653)
+//   unreadable file      -> stdout message, exit 0           (main.cpp:567)
+//   missing command      -> stdout "Error: Requires ...", 0  (main.cpp:574-602)
+//   bad command          -> std::cerr lines, uncaught exception (abort)
+// New optional flags (the reference has none): --depth N, --imsize W H,
+// --gpus N (row strips rendered on N devices concurrently), --device D,
+// --float-out FILE (raw float32 H*W*3 framebuffer), --stats.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rt_hip.h"
+#include "rt_host.h"
+
+int main(int argc, char *argv[]) {
+    if (argc <= 1) {
+        std::cout << "Error: Incorrect number of arguments in input file. Please follow this formate: imsize width height"
+                  << std::endl;
+        return 0;
+    }
+    int depth = -1, W = -1, H = -1, gpus = 1, device = 0;
+    bool stats = false;
+    const char *float_out = nullptr;
+    for (int i = 2; i < argc; i++) {
+        std::string a = argv[i];
+        if (a == "--depth" && i + 1 < argc) depth = atoi(argv[++i]);
+        else if (a == "--imsize" && i + 2 < argc) W = atoi(argv[++i]), H = atoi(argv[++i]);
+        else if (a == "--gpus" && i + 1 < argc) gpus = atoi(argv[++i]);
+        else if (a == "--device" && i + 1 < argc) device = atoi(argv[++i]);
+        else if (a == "--float-out" && i + 1 < argc) float_out = argv[++i];
+        else if (a == "--stats") stats = true;
+    }
+    rth_scene *hs = nullptr;
+    std::vector<char> msg(1 << 16);
+    int rc = rth_parse_file(argv[1], &hs, msg.data(), (int)msg.size());
+    if (rc > 0) {
+        std::cout << msg.data() << std::endl;
+        return 0;
+    }
+    if (rc < 0) {
+        std::string m(msg.data());
+        size_t cut = m.rfind('\n');
+        if (cut != std::string::npos) std::cerr << m.substr(0, cut) << std::endl;
+        std::string what = cut == std::string::npos ? m : m.substr(cut + 1);
+        if (rc == -2) throw std::out_of_range(what);
+        throw std::invalid_argument(what);
+    }
+    if (depth >= 0) rth_set_depth(hs, depth);
+    if (W > 1 && H > 1) rth_set_imsize(hs, W, H);
+    W = rth_width(hs);
+    H = rth_height(hs);
+    rt_camera cam;
+    rth_camera(hs, W, H, &cam);
+
+    int ndev = rt_device_count();
+    if (ndev < 1) {
+        std::cerr << "rt: no HIP device" << std::endl;
+        return 2;
+    }
+    if (gpus < 1) gpus = 1;
+    if (gpus > ndev - device) gpus = ndev - device;
+    std::vector<float> img((size_t)W * H * 3);
+    std::vector<rt_stats> st(gpus);
+    std::vector<int> rcs(gpus, 0);
+    std::vector<std::thread> pool;
+    for (int g = 0; g < gpus; g++) {
+        pool.emplace_back([&, g] {
+            int y0 = (int)((long long)H * g / gpus), y1 = (int)((long long)H * (g + 1) / gpus);
+            rt_scene *s = nullptr;
+            int r = rt_scene_create(device + g, rth_desc(hs), &s);
+            if (!r) r = rt_render_rows(s, &cam, W, H, y0, y1, img.data() + (size_t)y0 * W * 3, &st[g]);
+            rt_scene_destroy(s);
+            rcs[g] = r;
+        });
+    }
+    for (auto &t : pool) t.join();
+    for (int g = 0; g < gpus; g++) {
+        if (rcs[g]) {
+            std::cerr << "rt: render failed on device " << device + g << ": " << rt_strerror(rcs[g]) << std::endl;
+            return 3;
+        }
+    }
+    if (stats) {
+        unsigned long long tot[4] = {0, 0, 0, 0};
+        double ms = 0;
+        for (auto &s : st) {
+            tot[0] += s.primary, tot[1] += s.shadow, tot[2] += s.refraction, tot[3] += s.reflection;
+            ms = std::max(ms, s.kernel_ms);
+        }
+        fprintf(stderr, "rays primary=%llu shadow=%llu refraction=%llu reflection=%llu kernel_ms=%.3f Mrays/s=%.1f\n",
+                tot[0], tot[1], tot[2], tot[3], ms, (tot[0] + tot[1] + tot[2] + tot[3]) / (ms * 1e3));
+    }
+    if (float_out) {
+        FILE *f = fopen(float_out, "wb");
+        if (f) {
+            fwrite(img.data(), sizeof(float), img.size(), f);
+            fclose(f);
+        }
+    }
+    char out[4096];
+    rth_output_path(argv[1], out, sizeof out);
+    if (rth_write_ppm(out, img.data(), W, H, 0) != 0) {
+        std::cout << "ERROR: failed to create ppm image" << std::endl;
+        return 0;
+    }
+    rth_free(hs);
+    return 0;
+}

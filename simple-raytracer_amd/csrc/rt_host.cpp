@@ -1,0 +1,564 @@
+// rt_host.cpp -- host front end of the MI355X renderer (librt_host.so).
+//
+// Drop-in for the parts of the reference that surround the hot path:
+//   scene parser      main.cpp:88-602, keyword table src/config.h:17-50
+//   P3 texture reader src/utility.h:59-139
+//   camera            main.cpp:677-710
+//   quantisation      main.cpp:760-762
+//   PPM writer        main.cpp:613-650, remove_extension src/utility.h:34-41
+//
+// The parser keeps the reference's observable quirks (see DESIGN.md §Front
+// end): tokens are split on single spaces and an empty token is fatal; a
+// command with no arguments or an unknown keyword (including '#') is ignored;
+// std::stof prefix parsing ("1git" -> 1); mtlcolor resets texture mode;
+// 'f' vertex formats are tried as v/t/n, v//n, v/t, v with sscanf and the
+// last vertex decides smooth shading; unknown v/vn/vt indices resolve to zero.
+// Where the reference reads past a std::vector (too few arguments) it has
+// undefined behaviour; here that is reported like a stof failure.
+#include "rt_host.h"
+
+#include <algorithm>
+#include <charconv>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// float semantics of src/definitions.h Vector3 (no FMA: built -ffp-contract=off)
+// ---------------------------------------------------------------------------
+struct F3 {
+    float x, y, z;
+};
+inline F3 add(F3 a, F3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline F3 sub(F3 a, F3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline F3 scale(F3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline F3 divs(F3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+inline float hsum(F3 a) { return a.x + a.y + a.z; }
+inline float dot(F3 a, F3 b) { return hsum({a.x * b.x, a.y * b.y, a.z * b.z}); }
+inline F3 unit(F3 a) { return divs(a, std::sqrt(dot(a, a))); }
+inline F3 cross(F3 a, F3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// A parse failure: the std::cerr lines the reference prints before the
+// exception escapes main(), and the escaping exception's what().
+struct ParseFailure {
+    std::vector<std::string> cerr_lines;
+    std::string what;
+    bool out_of_range;
+};
+
+struct Fatal : std::exception {
+    ParseFailure f;
+};
+
+[[noreturn]] void fail(std::vector<std::string> lines, std::string what, bool oor = false) {
+    Fatal e;
+    e.f = {std::move(lines), std::move(what), oor};
+    throw e;
+}
+
+}  // namespace
+
+struct rth_scene {
+    std::vector<rt_sphere_desc> spheres;
+    std::vector<rt_face_desc> faces;
+    std::vector<rt_light_desc> lights;
+    std::vector<std::vector<unsigned char>> texels;
+    std::vector<rt_texture_desc> textures;
+    rt_scene_desc desc{};
+    F3 eye{}, viewdir{}, updir{};
+    float fov = 0;
+    int width = 0, height = 0;
+
+    void finalize() {
+        desc.n_spheres = (int)spheres.size();
+        desc.spheres = spheres.data();
+        desc.n_faces = (int)faces.size();
+        desc.faces = faces.data();
+        desc.n_lights = (int)lights.size();
+        desc.lights = lights.data();
+        for (size_t i = 0; i < textures.size(); i++) textures[i].rgb = texels[i].data();
+        desc.n_textures = (int)textures.size();
+        desc.textures = textures.data();
+    }
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// read_texture (src/utility.h:59-139): P3 only, maxval token must be "255",
+// '#' lines skipped, an empty line throws (line.at(0)), tokens split on ' '.
+// ---------------------------------------------------------------------------
+void load_p3(const std::string &path, int &w, int &h, std::vector<unsigned char> &rgb) {
+    std::ifstream in(path, std::ios::binary);
+    std::string data;
+    if (in) {
+        std::ostringstream ss;
+        ss << in.rdbuf();
+        data = ss.str();
+    } else {
+        throw std::runtime_error("cannot open texture '" + path + "'");
+    }
+    size_t ntok = 0, need = 0, got = 0;
+    w = h = 0;
+    const char *p = data.data(), *end = p + data.size();
+    while (p < end) {
+        const char *nl = static_cast<const char *>(memchr(p, '\n', (size_t)(end - p)));
+        const char *le = nl ? nl : end;
+        if (le == p) throw std::out_of_range("basic_string::at: __n (which is 0) >= this->size() (which is 0)");
+        if (*p != '#') {
+            const char *q = p;
+            while (q < le) {
+                const char *t = q;
+                while (t < le && *t != ' ') t++;
+                if (t > q) {
+                    std::string tok(q, t);
+                    ntok++;
+                    if (ntok == 1) {
+                        if (tok != "P3") throw std::invalid_argument("Only supports PPM 'P3' file format.");
+                    } else if (ntok == 2) {
+                        w = std::stoi(tok);
+                    } else if (ntok == 3) {
+                        h = std::stoi(tok);
+                        if (w > 0 && h > 0) {
+                            need = (size_t)w * (size_t)h * 3;
+                            rgb.assign(need, 0);
+                        }
+                    } else if (ntok == 4) {
+                        if (tok != "255") throw std::invalid_argument("PPM pixel value must be between 0 - 255 .");
+                    } else {
+                        int v = std::stoi(tok);
+                        if (got < need) rgb[got] = (unsigned char)std::clamp(v, 0, 255);
+                        got++;
+                    }
+                }
+                q = t + 1;
+            }
+        }
+        p = le + 1;
+    }
+    if (w <= 0 || h <= 0 || got < need) throw std::out_of_range("vector::_M_range_check");
+}
+
+float stof_or(const std::vector<std::string> &a, size_t i) {
+    if (i >= a.size()) throw std::invalid_argument("stof");
+    return std::stof(a[i]);
+}
+
+enum Cmd { EYE, VIEWDIR, UPDIR, HFOV, IMSIZE, BKGCOLOR, MTLCOLOR, TEXTURE, SPHERE, LIGHT, V, VN, VT, FACE };
+
+const std::pair<const char *, Cmd> kKeywords[] = {
+    {"eye", EYE},     {"viewdir", VIEWDIR}, {"updir", UPDIR},     {"hfov", HFOV},       {"imsize", IMSIZE},
+    {"bkgcolor", BKGCOLOR}, {"mtlcolor", MTLCOLOR}, {"texture", TEXTURE}, {"sphere", SPHERE},
+    {"light", LIGHT}, {"v", V},             {"vn", VN},           {"vt", VT},           {"f", FACE},
+};
+
+bool lookup(const std::string &s, Cmd &c) {
+    for (auto &kv : kKeywords)
+        if (s == kv.first) {
+            c = kv.second;
+            return true;
+        }
+    return false;
+}
+
+struct Parser {
+    rth_scene &S;
+    std::vector<F3> verts, norms;
+    std::vector<std::pair<float, float>> uvs;
+    rt_material cur{};
+    bool have_mtl = false, textured = false;
+    int cur_tex = -1;
+    bool seen[6] = {};
+
+    explicit Parser(rth_scene &s) : S(s) {}
+
+    static F3 lookup3(const std::vector<F3> &v, unsigned idx) {
+        return (idx >= 1 && idx <= v.size()) ? v[idx - 1] : F3{0, 0, 0};
+    }
+
+    // each case mirrors a 'case ArgValues::...' of main.cpp:141-556; `inner`
+    // is the message the case's own catch prints before rethrowing.
+    void vec3_cmd(const std::vector<std::string> &a, F3 &dst, const char *name) {
+        try {
+            dst = {stof_or(a, 0), stof_or(a, 1), stof_or(a, 2)};
+        } catch (const std::exception &e) {
+            fail({e.what(), std::string("ERROR: Invalid args for '") + name + "' command. Please verify."}, "");
+        }
+    }
+
+    void material_cmd(const std::vector<std::string> &a) {
+        textured = false;
+        rt_material m{};
+        try {
+            for (int i = 0; i < 3; i++) m.diffuse[i] = stof_or(a, i);
+            for (int i = 0; i < 3; i++) m.specular[i] = stof_or(a, 3 + i);
+            m.ka = stof_or(a, 6);
+            m.kd = stof_or(a, 7);
+            m.ks = stof_or(a, 8);
+            m.n = stof_or(a, 9);
+            if (a.size() == 12) {
+                m.opacity = std::clamp<float>(stof_or(a, 10), 0.0f, 1.0f);
+                m.eta = stof_or(a, 11);
+            } else {
+                m.opacity = 1.0f;
+                m.eta = 1.0f;
+            }
+        } catch (const std::exception &e) {
+            fail({e.what(), "ERROR: Issue parsing 'material' from arguments. Please verify."}, "");
+        }
+        cur = m;
+        have_mtl = true;
+    }
+
+    void attach_material(rt_material &m, int &tex, std::vector<std::string> &why) {
+        m = cur;
+        tex = -1;
+        if (textured) {
+            if (!have_mtl || cur_tex < 0) {
+                why = {"ERROR: Must define a 'mtlcolor' and 'texture'. Please verify."};
+                return;
+            }
+            tex = cur_tex;
+        } else if (!have_mtl) {
+            why = {"ERROR: Must define a 'mtlcolor'. Please verify."};
+        }
+    }
+
+    void sphere_cmd(const std::vector<std::string> &a) {
+        rt_sphere_desc s{};
+        try {
+            s.radius = stof_or(a, 3);
+            s.center[0] = stof_or(a, 0);
+            s.center[1] = stof_or(a, 1);
+            s.center[2] = stof_or(a, 2);
+        } catch (const std::exception &e) {
+            fail({e.what(), "ERROR: Invalid args for 'sphere' object. Please verify."}, "");
+        }
+        std::vector<std::string> why;
+        attach_material(s.mat, s.texture, why);
+        if (!why.empty()) {
+            why.push_back("ERROR: Invalid args for 'mtlcolor' command. Please verify.");
+            fail(why, "");
+        }
+        S.spheres.push_back(s);
+    }
+
+    void face_cmd(const std::vector<std::string> &a) {
+        rt_face_desc f{};
+        std::vector<std::string> why;
+        for (int i = 0; i < 3; i++) {
+            // main.cpp:487-517: formats tried in this order; the last vertex
+            // token decides smooth shading
+            unsigned v = 0, t = 0, n = 0;
+            int fmt = 0;  // 1 v/t/n, 2 v//n, 3 v/t, 4 v
+            if ((size_t)i < a.size()) {
+                const char *s = a[i].c_str();
+                if (sscanf(s, "%d/%d/%d", (int *)&v, (int *)&t, (int *)&n) == 3) fmt = 1;
+                else if (sscanf(s, "%d//%d", (int *)&v, (int *)&n) == 2) fmt = 2;
+                else if (sscanf(s, "%d/%d", (int *)&v, (int *)&t) == 2) fmt = 3;
+                else if (sscanf(s, "%d", (int *)&v) == 1) fmt = 4;
+            }
+            if (fmt == 0) {
+                why = {"ERROR: Invalid args for 'f' object. Please verify."};
+                break;
+            }
+            F3 pv = lookup3(verts, v);
+            f.v[i][0] = pv.x, f.v[i][1] = pv.y, f.v[i][2] = pv.z;
+            f.smooth = (fmt == 1 || fmt == 2) ? 1 : 0;
+            if (fmt == 1 || fmt == 2) {
+                F3 pn = lookup3(norms, n);
+                f.vn[i][0] = pn.x, f.vn[i][1] = pn.y, f.vn[i][2] = pn.z;
+            }
+            if (fmt == 1 || fmt == 3) {
+                bool ok = t >= 1 && t <= uvs.size();
+                f.vt[i][0] = ok ? uvs[t - 1].first : 0.0f;
+                f.vt[i][1] = ok ? uvs[t - 1].second : 0.0f;
+            }
+        }
+        if (why.empty()) attach_material(f.mat, f.texture, why);
+        if (!why.empty()) {
+            why.push_back("ERROR: Invalid args for 'f' (face) object. Please verify.");
+            fail(why, "");
+        }
+        S.faces.push_back(f);
+    }
+
+    void line(const std::string &text) {
+        // tokenise exactly like main.cpp:107-117
+        std::vector<std::string> tok;
+        size_t pos = 0;
+        while (pos < text.size()) {
+            size_t sp = text.find(' ', pos);
+            if (sp == std::string::npos) sp = text.size();
+            if (sp == pos) fail({}, "basic_string::at: __n (which is 0) >= this->size() (which is 0)", true);
+            tok.emplace_back(text, pos, sp - pos);
+            pos = sp + 1;
+        }
+        if (tok.empty()) return;
+        const std::string name = tok.front();
+        std::vector<std::string> a(tok.begin() + 1, tok.end());
+        Cmd c;
+        if (a.empty() || !lookup(name, c)) return;
+        try {
+            dispatch(c, a);
+        } catch (Fatal &e) {
+            // main.cpp:558-561: every failure is reported as an unknown command
+            e.f.what = "ERROR: Command '" + name + "' is undefined. Please verify input.";
+            throw;
+        }
+    }
+
+    void dispatch(Cmd c, const std::vector<std::string> &a) {
+        switch (c) {
+            case EYE: seen[1] = true; vec3_cmd(a, S.eye, "eye"); break;
+            case VIEWDIR: seen[2] = true; vec3_cmd(a, S.viewdir, "viewdir"); break;
+            case UPDIR: seen[3] = true; vec3_cmd(a, S.updir, "updir"); break;
+            case HFOV:
+                seen[4] = true;
+                try {
+                    S.fov = stof_or(a, 0);
+                } catch (const std::exception &e) {
+                    fail({e.what(), "ERROR: Invalid args for 'hfov' command. Please verify."}, "");
+                }
+                break;
+            case IMSIZE: {
+                seen[0] = true;
+                const char *msg = "ERROR: Invalid image dimensions. Please verify.";
+                int w = 0, h = 0;
+                try {
+                    if (a.size() < 2) throw std::invalid_argument("stoi");
+                    h = std::stoi(a[1]);
+                    w = std::stoi(a[0]);
+                } catch (const std::exception &e) {
+                    fail({e.what(), msg}, "");
+                }
+                if (h <= 1 || w <= 1) fail({msg}, "");
+                S.width = w;
+                S.height = h;
+                break;
+            }
+            case BKGCOLOR:
+                seen[5] = true;
+                try {
+                    for (int i = 0; i < 3; i++) S.desc.bkg[i] = stof_or(a, i);
+                    if (a.size() > 3) S.desc.eta_bkg = std::stof(a[3]);
+                } catch (const std::exception &e) {
+                    fail({e.what(), "ERROR: Invalid args for 'bkgcolor' command. Please verify."}, "");
+                }
+                break;
+            case MTLCOLOR: material_cmd(a); break;
+            case TEXTURE: {
+                textured = true;
+                int w = 0, h = 0;
+                std::vector<unsigned char> rgb;
+                try {
+                    load_p3(a[0], w, h, rgb);
+                } catch (const std::exception &e) {
+                    fail({e.what(), "ERROR: Issue reading 'texture' from ppm. Please verify."}, "");
+                }
+                S.texels.push_back(std::move(rgb));
+                S.textures.push_back({w, h, nullptr});
+                cur_tex = (int)S.textures.size() - 1;
+                break;
+            }
+            case SPHERE: sphere_cmd(a); break;
+            case LIGHT: {
+                rt_light_desc l{};
+                try {
+                    l.w = stof_or(a, 3);
+                    for (int i = 0; i < 3; i++) l.xyz[i] = stof_or(a, i);
+                    for (int i = 0; i < 3; i++) l.color[i] = stof_or(a, 4 + i);
+                } catch (const std::exception &e) {
+                    fail({e.what(), "ERROR: Invalid args for 'light' command. Please verify."}, "");
+                }
+                S.lights.push_back(l);
+                break;
+            }
+            case V:
+            case VN: {
+                F3 p{};
+                try {
+                    p = {stof_or(a, 0), stof_or(a, 1), stof_or(a, 2)};
+                } catch (const std::exception &e) {
+                    fail({e.what(), c == V ? "ERROR: Invalid args for vertex. Please verify."
+                                           : "ERROR: Invalid args for vertex normal. Please verify."},
+                         "");
+                }
+                (c == V ? verts : norms).push_back(p);
+                break;
+            }
+            case VT: {
+                std::pair<float, float> t;
+                try {
+                    t = {stof_or(a, 0), stof_or(a, 1)};
+                } catch (const std::exception &e) {
+                    fail({e.what(), "ERROR: Invalid args for texture coordinate. Please verify."}, "");
+                }
+                uvs.push_back(t);
+                break;
+            }
+            case FACE: face_cmd(a); break;
+        }
+    }
+};
+
+void copy_msg(char *msg, int msglen, const std::string &s) {
+    if (!msg || msglen <= 0) return;
+    size_t n = std::min((size_t)msglen - 1, s.size());
+    memcpy(msg, s.data(), n);
+    msg[n] = 0;
+}
+
+// main.cpp:760 on x86-64 (cvttss2si): NaN and out-of-range -> INT_MIN
+inline long long quantize1(float c) {
+    float x = (c - 0.0f) * (255.0f - 0.0f) / (1.0f - 0.0f) + 0.0f;
+    if (x >= -2147483648.0f && x < 2147483648.0f) return (long long)(int)x;
+    return (long long)INT_MIN;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rth_parse_file(const char *path, rth_scene **out, char *msg, int msglen) {
+    *out = nullptr;
+    std::ifstream in(path);
+    if (!in.is_open()) {
+        copy_msg(msg, msglen,
+                 std::string("ERROR: Issue reading input file '") + path + "'. Please verify path.");
+        return 1;
+    }
+    auto *S = new rth_scene();
+    S->desc.epsilon = 1.0e-3f;  // main.cpp:101
+    S->desc.depth = 4;          // main.cpp:100
+    S->desc.eta_bkg = 0.0f;     // main.cpp:751 default-insert
+    Parser P(*S);
+    std::string text;
+    try {
+        while (std::getline(in, text)) P.line(text);
+    } catch (Fatal &e) {
+        std::string s;
+        for (auto &l : e.f.cerr_lines) s += l + "\n";
+        s += e.f.what;
+        copy_msg(msg, msglen, s);
+        delete S;
+        return e.f.out_of_range ? -2 : -1;
+    }
+    static const char *need[] = {"imsize", "eye", "viewdir", "updir", "hfov", "bkgcolor"};
+    for (int i = 0; i < 6; i++) {
+        if (!P.seen[i]) {
+            copy_msg(msg, msglen, std::string("Error: Requires command '") + need[i] + "'");
+            delete S;
+            return 1;
+        }
+    }
+    S->finalize();
+    *out = S;
+    return 0;
+}
+
+void rth_free(rth_scene *s) { delete s; }
+const rt_scene_desc *rth_desc(const rth_scene *s) { return &s->desc; }
+void rth_set_depth(rth_scene *s, int depth) { s->desc.depth = depth; }
+void rth_set_imsize(rth_scene *s, int w, int h) {
+    s->width = w;
+    s->height = h;
+}
+int rth_width(const rth_scene *s) { return s->width; }
+int rth_height(const rth_scene *s) { return s->height; }
+
+// main.cpp:607 (normalised view vectors) + :677-710
+int rth_camera(const rth_scene *s, int W, int H, rt_camera *cam) {
+    if (!s || !cam || W < 2 || H < 2) return RT_E_INVALID;
+    const double kPi = 3.14159265358979323846;  // src/config.h:11
+    const double kD = 5.0;                      // src/config.h:8
+    F3 n = unit(s->viewdir), up = unit(s->updir);
+    float res_w = (float)W, res_h = (float)H;
+    F3 u = unit(cross(n, up));
+    F3 v = cross(u, n);
+    float aspect = res_w / res_h;
+    float w = (float)(2.0f * kD * std::tan((0.5 * (double)s->fov) * kPi / 180.0f));
+    float h = w / aspect;
+    F3 c = add(s->eye, scale(n, (float)kD));
+    F3 half_u = scale(u, w / 2.0f), half_v = scale(v, h / 2.0f);
+    F3 ul = add(sub(c, half_u), half_v);
+    F3 ur = add(add(c, half_u), half_v);
+    F3 ll = sub(sub(c, half_u), half_v);
+    F3 dh = divs(sub(ur, ul), res_w - 1.0f);
+    F3 dv = divs(sub(ll, ul), res_h - 1.0f);
+    F3 *dst[4] = {(F3 *)cam->eye, (F3 *)cam->ul, (F3 *)cam->dh, (F3 *)cam->dv};
+    F3 src[4] = {s->eye, ul, dh, dv};
+    for (int i = 0; i < 4; i++) memcpy(dst[i], &src[i], sizeof(F3));
+    return RT_OK;
+}
+
+void rth_quantize(const float *rgb, long long n, long long *out) {
+    for (long long i = 0; i < n; i++) out[i] = quantize1(rgb[i]);
+}
+
+// main.cpp:628-648: the std::to_string of each size_t, parallel formatting
+int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads) {
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    fprintf(f, "P3 \n%d %d \n255 \n", W, H);
+    const size_t npx = (size_t)W * (size_t)H;
+    if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+    const size_t chunk = 1 << 16;
+    const size_t nchunks = (npx + chunk - 1) / chunk;
+    size_t next = 0;
+    int rc = 0;
+    while (next < nchunks) {
+        size_t batch = std::min(nchunks - next, (size_t)threads * 4);
+        std::vector<std::string> bufs(batch);
+        std::vector<std::thread> pool;
+        auto work = [&](size_t t0) {
+            for (size_t b = t0; b < batch; b += (size_t)threads) {
+                size_t p0 = (next + b) * chunk, p1 = std::min(npx, p0 + chunk);
+                std::string &s = bufs[b];
+                s.resize((p1 - p0) * 3 * 22);
+                char *o = s.data();
+                for (size_t p = p0; p < p1; p++) {
+                    for (int k = 0; k < 3; k++) {
+                        unsigned long long v = (unsigned long long)quantize1(rgb[p * 3 + k]);
+                        o = std::to_chars(o, o + 21, v).ptr;
+                        *o++ = ' ';
+                    }
+                    *o++ = '\n';
+                }
+                s.resize((size_t)(o - s.data()));
+            }
+        };
+        int nt = (int)std::min<size_t>((size_t)threads, batch);
+        for (int t = 1; t < nt; t++) pool.emplace_back(work, (size_t)t);
+        work(0);
+        for (auto &th : pool) th.join();
+        for (auto &s : bufs)
+            if (fwrite(s.data(), 1, s.size(), f) != s.size()) rc = -1;
+        next += batch;
+    }
+    if (fclose(f) != 0) rc = -1;
+    return rc;
+}
+
+int rth_output_path(const char *scene_path, char *out, int outlen) {
+    std::string s(scene_path);
+    size_t dot = s.rfind('.');
+    if (dot != std::string::npos) s.resize(dot);
+    s += ".ppm";
+    if ((int)s.size() + 1 > outlen) return -1;
+    memcpy(out, s.c_str(), s.size() + 1);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1038 @@
+// rt_kernels.hip -- MI355X (gfx950) ray-trace kernel + the C ABI of rt_hip.h.
+//
+// Replaces the reference's hot path: the pixel loop main.cpp:718-764, TraceRay
+// main.cpp:1215-1407 and ShadeRay main.cpp:783-1207 (called recursively).
+//
+// Execution model:
+//  * persistent workgroups; every lane owns one pixel at a time and walks
+//    that pixel's ShadeRay tree as an explicit state machine (frames in
+//    scratch), one TraceRay-equivalent scan per loop iteration;
+//  * all active lanes of a wave scan the primitive list together (uniform
+//    loop, primitive data broadcast from LDS or scalar-loaded), whatever kind
+//    of ray each lane carries (primary / shadow / refraction / reflection);
+//  * a lane that finishes its pixel is refilled in the same iteration: the
+//    wave ballots its idle lanes, one lane takes a block of pixel indices with
+//    a single atomicAdd and each idle lane picks its own by a prefix count of
+//    the ballot (mbcnt) -- wave-level ballot/prefix compaction of the work;
+//  * scene arrays are staged once per workgroup into LDS when they fit,
+//    otherwise read through the scalar cache;
+//  * framebuffer: 12 B/pixel fp32 RGB stores (pre-quantisation colour).
+//
+// Numerics follow the reference operation by operation (built with
+// -ffp-contract=off, correctly rounded div/sqrt, std::clamp-style compares,
+// the reference's double-precision intermediates where they change the
+// result).  Two documented relaxations: the sphere C and discriminant use one
+// fmaf each instead of the reference's double expression (identical except for
+// a double-rounding tie, ~2^-29 per test), and libm (glibc) vs ocml
+// powf/acosf/asinf/acos/atan2 differences.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_hip.h"
+
+namespace rt {
+
+// ---------------------------------------------------------------------------
+// Device-side geometry/colour semantics of src/definitions.h
+// ---------------------------------------------------------------------------
+struct V3 {
+    float x, y, z;
+};
+struct C3 {
+    float r, g, b;
+};
+
+__host__ __device__ __forceinline__ V3 vadd(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__host__ __device__ __forceinline__ V3 vsub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__host__ __device__ __forceinline__ V3 vmul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__host__ __device__ __forceinline__ V3 vdiv(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__host__ __device__ __forceinline__ float vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ V3 vnorm(V3 a) { return vdiv(a, sqrtf(vdot(a, a))); }
+__host__ __device__ __forceinline__ V3 vcross(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+// std::clamp(v, 0, 1): NaN passes through (not fminf/fmaxf)
+__device__ __forceinline__ float clamp01(float v) { return (v < 0.0f) ? 0.0f : ((1.0f < v) ? 1.0f : v); }
+__device__ __forceinline__ float clampr(float v, float lo, float hi) { return (v < lo) ? lo : ((hi < v) ? hi : v); }
+__device__ __forceinline__ C3 cmulc(C3 a, C3 b) { return {clamp01(b.r * a.r), clamp01(b.g * a.g), clamp01(b.b * a.b)}; }
+__device__ __forceinline__ C3 cmulf(C3 a, float f) { return {clamp01(f * a.r), clamp01(f * a.g), clamp01(f * a.b)}; }
+__device__ __forceinline__ C3 cadd(C3 a, C3 b) { return {clamp01(b.r + a.r), clamp01(b.g + a.g), clamp01(b.b + a.b)}; }
+__device__ __forceinline__ float max0(float x) { return (0.0f < x) ? x : 0.0f; }
+
+constexpr double kPi = 3.14159265358979323846;        // src/config.h:11
+constexpr double kRightAngle = 90.0 * kPi / 180.0;    // main.cpp:964
+constexpr float kFltMax = 3.40282347e+38f;            // std::numeric_limits<float>::max()
+
+enum { ENTERING = 0, EXITING = 1 };
+
+// ---------------------------------------------------------------------------
+// Device scene layout (built by rt_scene_create)
+// ---------------------------------------------------------------------------
+// Faces (object index 0..nf-1), 5 x float4 each, per-face invariants hoisted
+// exactly as TraceRay computes them (main.cpp:1280-1301, :1361-1366):
+//   [0] v0.xyz, D = -n.v0     [1] n.xyz, det = d11*d22 - d12*d12
+//   [2] e1.xyz, d11           [3] e2.xyz, d22        [4] d12, -, -, -
+// Spheres (object index nf..nf+ns-1): float4 center.xyz, radius.
+struct ObjK {                 // per object, shading data
+    float dif[3], ka;
+    float spc[3], kd;
+    float ks, n, opacity, eta;
+    int tex;                  // texture index or -1
+    int is_sphere;
+    int pad[2];
+};
+struct FaceShadeK {           // per face, shading-only data
+    float vn[3][3];           // vertex_normal[k].norm() (main.cpp:1382-1384)
+    float vt[3][2];           // clamp<float>(texture_coords, 0, 1) (main.cpp:835-841)
+    int smooth;
+    int pad[2];
+};
+struct LightK {
+    float xyz[3], w;          // position or direction, w
+    float col[3], pad0;
+    float L[3], pad1;         // directional: light.direction.norm() * -1 (main.cpp:887)
+    float sdir[3], pad2;      // directional: light.direction * -1 (main.cpp:895, unnormalised)
+};
+struct TexK {
+    int w, h;
+    long long off;
+};
+
+struct Params {
+    const float4 *__restrict__ fscan;
+    const float4 *__restrict__ sscan;
+    const float *__restrict__ ofac;      // (float)(1.0 - opacity) per object (main.cpp:909)
+    const ObjK *__restrict__ objs;
+    const FaceShadeK *__restrict__ fsh;
+    const LightK *__restrict__ lights;
+    const unsigned char *__restrict__ texels;
+    const TexK *__restrict__ texs;
+    float *__restrict__ out;
+    unsigned int *__restrict__ work;     // pixel work counter
+    unsigned long long *__restrict__ stats;
+    int nf, ns, nl;
+    float bkg[3];
+    float eta_bkg, eps;
+    int depth;
+    float eye[3], ul[3], dh[3], dv[3];
+    int W, y0, rows;                     // render rows [y0, y0 + rows) of a W-wide image
+    unsigned int total;                  // W * rows
+};
+
+// ---------------------------------------------------------------------------
+// One lane's ray query (a TraceRay call + the consumer loop that follows it)
+// ---------------------------------------------------------------------------
+//  closest : smallest t with tmin < t < running min, ties -> first in order
+//            (main.cpp:732-742, :992-1011, :1113-1124); skipchk applies the
+//            SKIP_TRANS rule (main.cpp:1000-1002) against object `back`
+//  shadow  : every intersection of every object != self with tmin < t (and
+//            t < tmax unless unbounded) multiplies mask by (1 - opacity)
+//            (main.cpp:898-912, :930-949)
+struct Query {
+    V3 o, d;
+    float tmin, tmax;
+    int self, back, win;
+    bool closest, unb, skipchk, skipped;
+    C3 mask;
+};
+
+constexpr float kInf = __builtin_huge_valf();
+
+__device__ __forceinline__ void offer(Query &q, float t, int obj, const float *__restrict__ ofac) {
+    bool in = (t > q.tmin) & ((t < q.tmax) | q.unb) & (obj != q.self);
+    if (in) {
+        if (q.closest) {
+            if (q.skipchk & (obj != q.back)) {
+                q.skipped = true;
+                q.tmin = kInf;               // 'goto SKIP_TRANS': the scan is over
+            } else {
+                q.tmax = t;
+                q.win = obj;
+            }
+        } else {
+            float f = ofac[obj];
+            q.mask = cmulf(q.mask, f);
+            // an opaque occluder zeroes the mask for good: any-hit termination
+            if ((q.mask.r == 0.0f) & (q.mask.g == 0.0f) & (q.mask.b == 0.0f)) q.tmin = kInf;
+        }
+    }
+}
+
+// TraceRay's face test (main.cpp:1296-1378); returns t if the ray hits the
+// triangle's open interior.
+__device__ __forceinline__ bool face_test(float4 f0, float4 f1, float4 f2, float4 f3, float4 f4, V3 o, V3 d,
+                                          float &t, float &a, float &b, float &g) {
+    V3 n = {f1.x, f1.y, f1.z};
+    float dem = vdot(n, d);
+    if (dem == 0.0f) return false;
+    V3 v0 = {f0.x, f0.y, f0.z};
+    t = -(vdot(n, o) + f0.w) / dem;
+    V3 ep = vsub(vadd(o, vmul(d, t)), v0);
+    V3 e1 = {f2.x, f2.y, f2.z}, e2 = {f3.x, f3.y, f3.z};
+    float d1p = vdot(e1, ep), d2p = vdot(e2, ep);
+    float d11 = f2.w, d22 = f3.w, d12 = f4.x, det = f1.w;
+    b = (d22 * d1p - d12 * d2p) / det;
+    g = (d11 * d2p - d12 * d1p) / det;
+    a = 1.0f - (b + g);
+    return (0.0f < a) & (a < 1.0f) & (0.0f < b) & (b < 1.0f) & (0.0f < g) & (g < 1.0f);
+}
+
+// TraceRay's sphere test (main.cpp:1225-1258): both roots, A = 1 assumed.
+__device__ __forceinline__ bool sphere_test(float4 s, V3 o, V3 d, float &t1, float &t2) {
+    V3 dir = {o.x - s.x, o.y - s.y, o.z - s.z};
+    float B = 2.0f * vdot(d, dir);
+    float C = fmaf(-s.w, s.w, vdot(dir, dir));      // (float)((double)|dir|^2 - (double)r*r)
+    float det = fmaf(B, B, -4.0f * C);              // (float)((double)B*B - 4.0*C)
+    if (__builtin_signbitf(det)) return false;
+    float sq = sqrtf(det);
+    t1 = (-B + sq) * 0.5f;
+    t2 = (-B - sq) * 0.5f;
+    return true;
+}
+
+// The scan every active lane of the wave runs together.  SRC_LDS: primitive
+// arrays were staged into LDS (lds_f, lds_s); otherwise global (scalar) loads.
+template <bool SRC_LDS>
+__device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s) {
+    const float4 *F = SRC_LDS ? lds_f : p.fscan;
+    const float4 *S = SRC_LDS ? lds_s : p.sscan;
+    for (int i = 0; i < p.nf; i++) {
+        float4 f0 = F[5 * i + 0], f1 = F[5 * i + 1], f2 = F[5 * i + 2], f3 = F[5 * i + 3], f4 = F[5 * i + 4];
+        if (f1.w == 0.0f) continue;                 // det == 0: never intersects (main.cpp:1367)
+        if (q.tmin < kInf) {
+            float t, a, b, g;
+            if (face_test(f0, f1, f2, f3, f4, q.o, q.d, t, a, b, g)) offer(q, t, i, p.ofac);
+        }
+    }
+    for (int i = 0; i < p.ns; i++) {
+        float4 s = S[i];
+        if (q.tmin < kInf) {
+            float t1, t2;
+            if (sphere_test(s, q.o, q.d, t1, t2)) {
+                offer(q, t1, p.nf + i, p.ofac);
+                offer(q, t2, p.nf + i, p.ofac);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ShadeRay as a per-lane state machine
+// ---------------------------------------------------------------------------
+enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4 };
+
+template <int MAXF>
+struct Frame {
+    int obj, state, depth, phase, light, sn;
+    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
+    float ei, et;                    // incidence / transmission refraction index
+    V3 P, N, I;                      // hit point, shading normal (flipped for spheres), I = -ray
+    float cosI;
+    C3 dif, mask, acc;               // diffuse, cumulative shadow mask, running colour
+    float Ft;                        // transmission Fresnel F (main.cpp:966)
+};
+
+struct Counters {
+    unsigned prim, shadow, refr, refl, skip, ub;
+};
+
+// Hit record of the winning intersection, recomputed exactly as TraceRay did.
+__device__ void hit_geometry(const Params &p, int obj, V3 o, V3 d, float t, V3 &P, V3 &N, V3 &bary) {
+    P = vadd(o, vmul(d, t));
+    if (obj < p.nf) {
+        const float4 *F = p.fscan + 5 * obj;
+        float4 f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4];
+        V3 ep = vsub(P, V3{f0.x, f0.y, f0.z});
+        V3 e1 = {f2.x, f2.y, f2.z}, e2 = {f3.x, f3.y, f3.z};
+        float d1p = vdot(e1, ep), d2p = vdot(e2, ep);
+        float b = (f3.w * d1p - f4.x * d2p) / f1.w;
+        float g = (f2.w * d2p - f4.x * d1p) / f1.w;
+        float a = 1.0f - (b + g);
+        bary = {a, b, g};
+        const FaceShadeK &fs = p.fsh[obj];
+        if (fs.smooth) {
+            V3 n0 = {fs.vn[0][0], fs.vn[0][1], fs.vn[0][2]};
+            V3 n1 = {fs.vn[1][0], fs.vn[1][1], fs.vn[1][2]};
+            V3 n2 = {fs.vn[2][0], fs.vn[2][1], fs.vn[2][2]};
+            N = vnorm(vadd(vadd(vmul(n0, a), vmul(n1, b)), vmul(n2, g)));
+        } else {
+            N = {f1.x, f1.y, f1.z};
+        }
+    } else {
+        float4 s = p.sscan[obj - p.nf];
+        N = vnorm(vdiv(vsub(P, V3{s.x, s.y, s.z}), s.w));
+        bary = {0, 0, 0};
+    }
+}
+
+__device__ __forceinline__ float texel(const Params &p, const TexK &t, int x, int y, int c) {
+    float v = (float)p.texels[t.off + ((long long)y * t.w + x) * 3 + c];
+    return (v - 0.0f) * (1.0f - 0.0f) / (255.0f - 0.0f) + 0.0f;   // map(v, 0, 255, 0, 1)
+}
+
+// ShadeRay prologue (main.cpp:785-872): diffuse / texture and the sphere
+// normal flip.  Leaves the frame ready for the light loop.
+template <int MAXF>
+__device__ void node_begin(const Params &p, Frame<MAXF> &f, V3 o, V3 d, float t) {
+    V3 P, N, bary;
+    hit_geometry(p, f.obj, o, d, t, P, N, bary);
+    const ObjK &ob = p.objs[f.obj];
+    V3 I = vmul(d, -1.0f);
+    float cosI = vdot(N, I);
+    C3 dif = {ob.dif[0], ob.dif[1], ob.dif[2]};
+    if (ob.tex >= 0) {
+        TexK tx = p.texs[ob.tex];
+        float width = (float)tx.w, height = (float)tx.h;
+        if (ob.is_sphere) {                                          // main.cpp:805-826
+            float v = (float)(acos((double)N.z) / kPi);
+            float phi = (float)atan2((double)N.y, (double)N.x);
+            float u = (phi - (float)-kPi) * (1.0f - 0.0f) / ((float)kPi - (float)-kPi) + 0.0f;
+            v = clampr(v, 0.0f, 1.0f);
+            u = clampr(u, 0.0f, 1.0f);
+            int i = (int)clampr((float)round(((double)height - 1.0) * (double)v), 0.0f,
+                                (float)((double)height - 1.0));
+            int j = (int)clampr((float)round(((double)width - 1.0) * (double)u), 0.0f,
+                                (float)((double)width - 1.0));
+            dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
+        } else {                                                     // main.cpp:834-861
+            const FaceShadeK &fs = p.fsh[f.obj];
+            float u = (bary.x * fs.vt[0][0]) + (bary.y * fs.vt[1][0]) + (bary.z * fs.vt[2][0]);
+            float v = (bary.x * fs.vt[0][1]) + (bary.y * fs.vt[1][1]) + (bary.z * fs.vt[2][1]);
+            v = clampr(v, 0.0f, 1.0f);
+            u = clampr(u, 0.0f, 1.0f);
+            int i = (int)clampr(roundf((width - 1.0f) * u), 0.0f, (float)((double)width - 1.0));
+            int j = (int)clampr(roundf((height - 1.0f) * v), 0.0f, (float)((double)height - 1.0));
+            dif = {texel(p, tx, i, j, 0), texel(p, tx, i, j, 1), texel(p, tx, i, j, 2)};
+        }
+    }
+    if ((double)cosI < 0.0 && ob.is_sphere) {                      // main.cpp:869-872
+        N = vmul(N, -1.0f);
+        cosI = vdot(N, I);
+    }
+    f.P = P;
+    f.N = N;
+    f.I = I;
+    f.cosI = cosI;
+    f.dif = dif;
+    f.mask = {1.0f, 1.0f, 1.0f};
+    f.acc = {0.0f, 0.0f, 0.0f};      // tmp_specular while lights run
+    f.light = 0;
+    f.phase = PH_LIGHT;
+}
+
+// Direction of light l's shadow ray and the L vector (main.cpp:885-928).
+__device__ __forceinline__ void light_vectors(const LightK &lt, V3 P, V3 &L, V3 &sdir, float &distL, bool &unb) {
+    if (lt.w == 0.0f) {
+        L = {lt.L[0], lt.L[1], lt.L[2]};
+        sdir = {lt.sdir[0], lt.sdir[1], lt.sdir[2]};
+        distL = 0.0f;
+        unb = true;
+    } else {
+        V3 pos = {lt.xyz[0], lt.xyz[1], lt.xyz[2]};
+        L = vnorm(vsub(pos, P));
+        V3 dl = vsub(P, pos);
+        distL = sqrtf(vdot(dl, dl));
+        sdir = L;
+        unb = false;
+    }
+}
+
+// (float)(F_0 + (1.0 - F_0) * powf(1.0 - cos, 5.0)), main.cpp:966 / :1104
+__device__ __forceinline__ float schlick(float F0, float cosI) {
+    float p5 = powf((float)(1.0 - (double)cosI), 5.0f);
+    return (float)((double)F0 + (1.0 - (double)F0) * (double)p5);
+}
+
+template <int MAXF>
+__device__ __forceinline__ bool in_stack(const Frame<MAXF> &f, int obj) {
+    bool in = false;
+    for (int q = 0; q < f.sn; q++) in |= (f.stack[q] == obj);
+    return in;
+}
+
+// Medium-stack transition for the refraction child (main.cpp:1021-1070).
+template <int MAXF>
+__device__ void refr_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit, Counters &cnt) {
+    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
+    int n = f.sn;
+    float hit_eta = p.objs[hit].eta;
+    if (f.state == ENTERING) {
+        if (hit == f.obj) {
+            c.state = EXITING;
+            if (n > 0) {
+                c.ei = p.objs[c.stack[n - 1]].eta;
+                n--;
+            } else {
+                c.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
+                cnt.ub++;
+            }
+            c.et = n > 0 ? p.objs[c.stack[n - 1]].eta : p.eta_bkg;
+            if (n > 0) n--;
+        } else {
+            c.state = ENTERING;
+            c.ei = f.et;
+            c.et = hit_eta;
+            c.stack[n++] = hit;
+        }
+    } else if (n > 0) {
+        if (!in_stack(f, hit)) {
+            c.state = ENTERING;
+            c.ei = f.et;
+            c.et = hit_eta;
+            c.stack[n++] = hit;
+        } else {
+            c.state = EXITING;
+            c.ei = f.et;
+            c.et = p.objs[c.stack[n - 1]].eta;
+            n--;
+        }
+    } else {
+        c.state = ENTERING;
+        c.ei = p.eta_bkg;
+        c.et = hit_eta;
+        c.stack[0] = hit;
+        n = 1;
+    }
+    c.sn = n;
+}
+
+// Medium-stack transition for the reflection child (main.cpp:1134-1182).
+template <int MAXF>
+__device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit) {
+    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
+    int n = f.sn;
+    float hit_eta = p.objs[hit].eta;
+    if (f.state == ENTERING) {
+        c.state = ENTERING;
+        c.ei = f.ei;
+        if (n > 0) {
+            if (!in_stack(f, hit)) {
+                c.et = hit_eta;
+                c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
+            } else {
+                c.et = p.objs[c.stack[n - 1]].eta;
+                n--;
+            }
+        } else {
+            c.et = hit_eta;
+            c.stack[0] = hit;
+            n = 1;
+        }
+    } else {
+        c.ei = f.ei;
+        if (hit == f.obj) {
+            c.state = EXITING;
+            c.et = f.et;
+        } else {
+            c.state = ENTERING;
+            c.et = hit_eta;
+            c.stack[n++] = hit;
+        }
+    }
+    c.sn = n;
+}
+
+// Lane state between scans.
+template <int MAXF>
+struct LaneState {
+    Frame<MAXF> fr[MAXF];
+    int top;                         // -1: primary ray pending
+};
+
+// Advance one lane after its scan: consume the result, run ShadeRay logic
+// until the next TraceRay (returns true with q set up) or until the pixel is
+// done (returns false with `color` set).
+template <int MAXF>
+__device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
+    const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
+    int top = ls.top;
+    // ---- consume the scan result ----
+    if (top < 0) {                                   // primary (main.cpp:729-758)
+        if (q.win < 0) {
+            color = bkg;
+            return false;
+        }
+        Frame<MAXF> &f = ls.fr[0];
+        f.obj = q.win;
+        f.ei = p.eta_bkg;
+        f.et = p.objs[q.win].eta;
+        f.sn = 1;
+        f.stack[0] = q.win;
+        f.state = ENTERING;
+        f.depth = p.depth;
+        node_begin(p, f, q.o, q.d, q.tmax);
+        top = 0;
+    } else {
+        Frame<MAXF> &f = ls.fr[top];
+        if (f.phase == PH_LIGHT) {                   // main.cpp:952-958
+            f.mask = q.mask;
+            const LightK &lt = p.lights[f.light];
+            V3 L, sd;
+            float dl;
+            bool unb;
+            light_vectors(lt, f.P, L, sd, dl, unb);
+            const ObjK &ob = p.objs[f.obj];
+            V3 H = vnorm(vadd(L, f.I));
+            C3 dc = cmulf(cmulf(f.dif, ob.kd), max0(vdot(f.N, L)));
+            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), powf(max0(vdot(f.N, H)), ob.n));
+            C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
+            f.acc = cadd(f.acc, cmulc(cmulc(lc, f.mask), cadd(dc, sc)));
+            f.light++;
+        } else if (f.phase == PH_REFR) {
+            const ObjK &ob = p.objs[f.obj];
+            if (q.skipped) {
+                cnt.skip++;                          // tmp_transparency stays 0
+                f.phase = PH_REFL;
+            } else if (q.win >= 0) {
+                Frame<MAXF> &c = ls.fr[top + 1];
+                refr_transition(p, f, c, q.win, cnt);
+                c.obj = q.win;
+                c.depth = f.depth - 1;
+                f.phase = PH_REFR_CHILD;
+                node_begin(p, c, q.o, q.d, q.tmax);
+                top++;
+            } else {
+                C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)ob.opacity));
+                f.acc = cadd(f.acc, tr);
+                f.phase = PH_REFL;
+            }
+        } else if (f.phase == PH_REFL) {
+            if (q.win >= 0) {
+                Frame<MAXF> &c = ls.fr[top + 1];
+                refl_transition(p, f, c, q.win);
+                c.obj = q.win;
+                c.depth = f.depth - 1;
+                f.phase = PH_REFL_CHILD;
+                node_begin(p, c, q.o, q.d, q.tmax);
+                top++;
+            } else {
+                // miss: refl = bkg * F_r; finish this node below
+                const ObjK &ob = p.objs[f.obj];
+                float F0 = (ob.eta - 1) / (ob.eta + 1);
+                float Fr = schlick(F0 * F0, f.cosI);
+                f.acc = cadd(f.acc, cmulf(bkg, Fr));
+                f.phase = PH_REFL_CHILD + 1;         // done
+            }
+        }
+    }
+    // ---- run the current frame forward ----
+    for (;;) {
+        Frame<MAXF> &f = ls.fr[top];
+        const ObjK &ob = p.objs[f.obj];
+        if (f.phase == PH_LIGHT) {
+            if (f.light < p.nl) {                    // shadow ray for light f.light
+                V3 L, sd;
+                float dl;
+                bool unb;
+                light_vectors(p.lights[f.light], f.P, L, sd, dl, unb);
+                q.o = f.P;
+                q.d = sd;
+                q.tmin = p.eps;
+                q.tmax = dl;
+                q.unb = unb;
+                q.self = f.obj;
+                q.closest = false;
+                q.skipchk = false;
+                q.skipped = false;
+                q.win = -1;
+                q.mask = f.mask;
+                cnt.shadow++;
+                ls.top = top;
+                return true;
+            }
+            // ambient + specular sum, then Fresnel / transmission (main.cpp:961-992)
+            f.acc = cadd(cmulf(f.dif, ob.ka), f.acc);
+            float snell = f.ei / f.et;
+            float crit = asinf(f.et / f.ei);
+            float inc = acosf(f.cosI);
+            bool tir = (crit < inc) && ((double)inc < kRightAngle);
+            float F0 = (f.et - f.ei) / (f.et + f.ei);
+            f.Ft = schlick(F0 * F0, f.cosI);
+            if (f.depth > 0 && !tir && (double)ob.opacity < 1.0 && ob.eta > 0) {
+                float k = sqrtf((float)(1.0 - (double)(snell * snell) * (1.0 - (double)(f.cosI * f.cosI))));
+                V3 T = vadd(vmul(vmul(f.N, -1.0f), k), vmul(vsub(vmul(f.N, f.cosI), f.I), snell));
+                q.o = f.P;
+                q.d = T;
+                q.tmin = p.eps;
+                q.tmax = kFltMax;
+                q.unb = false;
+                q.self = -1;
+                q.closest = true;
+                q.skipchk = (f.sn > 0) && !ob.is_sphere;
+                q.back = f.sn > 0 ? f.stack[f.sn - 1] : -1;
+                q.skipped = false;
+                q.win = -1;
+                cnt.refr++;
+                f.phase = PH_REFR;
+                ls.top = top;
+                return true;
+            }
+            f.phase = PH_REFL;
+        }
+        if (f.phase == PH_REFL) {                    // main.cpp:1103-1124
+            float F0 = (ob.eta - 1) / (ob.eta + 1);
+            float Fr = schlick(F0 * F0, f.cosI);
+            if (f.depth > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
+                V3 R = vsub(vmul(f.N, (float)(2.0 * (double)f.cosI)), f.I);
+                q.o = f.P;
+                q.d = R;
+                q.tmin = p.eps;
+                q.tmax = kFltMax;
+                q.unb = false;
+                q.self = -1;
+                q.closest = true;
+                q.skipchk = false;
+                q.skipped = false;
+                q.win = -1;
+                cnt.refl++;
+                ls.top = top;
+                return true;
+            }
+            f.phase = PH_REFL_CHILD + 1;
+        }
+        // node complete: ((dka + spec) + trans) + refl already folded into acc
+        C3 c = f.acc;
+        if (top == 0) {
+            color = c;
+            ls.top = -1;
+            return false;
+        }
+        top--;
+        Frame<MAXF> &pf = ls.fr[top];
+        const ObjK &pob = p.objs[pf.obj];
+        if (pf.phase == PH_REFR_CHILD) {             // main.cpp:1072-1083
+            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)pf.Ft)), (float)(1.0 - (double)pob.opacity));
+            pf.acc = cadd(pf.acc, tr);
+            pf.phase = PH_REFL;
+        } else {                                     // PH_REFL_CHILD, main.cpp:1184-1194
+            float F0 = (pob.eta - 1) / (pob.eta + 1);
+            float Fr = schlick(F0 * F0, pf.cosI);
+            pf.acc = cadd(pf.acc, cmulf(c, Fr));
+            pf.phase = PH_REFL_CHILD + 1;
+        }
+    }
+}
+
+// Pixel index -> (x, y): strips of 8 rows, 8x8 blocks along the strip, so a
+// wave's 64 consecutive indices cover an 8x8 tile.
+__device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, int &y) {
+    unsigned strip_px = (unsigned)p.W * 8u;
+    unsigned s = idx / strip_px;
+    unsigned r = idx - s * strip_px;
+    int sh = min(8, p.rows - (int)s * 8);
+    x = (int)(r / (unsigned)sh);
+    y = (int)s * 8 + (int)(r % (unsigned)sh);
+}
+
+template <int MAXF, bool SRC_LDS>
+__global__ void __launch_bounds__(256) render_kernel(Params p) {
+    extern __shared__ float4 lds[];
+    const float4 *lds_f = lds;
+    const float4 *lds_s = lds + 5 * p.nf;
+    if (SRC_LDS) {
+        int nf4 = 5 * p.nf, ns4 = p.ns;
+        for (int i = threadIdx.x; i < nf4; i += blockDim.x) lds[i] = p.fscan[i];
+        for (int i = threadIdx.x; i < ns4; i += blockDim.x) lds[nf4 + i] = p.sscan[i];
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    LaneState<MAXF> ls;
+    ls.top = -1;
+    Counters cnt = {0, 0, 0, 0, 0, 0};
+    Query q;
+    bool busy = false;         // lane owns a pixel
+    bool pending = false;      // q holds a finished scan to consume
+    bool drained = false;      // wave saw the work counter run out
+    int px = 0, py = 0;
+    for (;;) {
+        if (pending) {
+            C3 color;
+            pending = advance<MAXF>(p, ls, q, cnt, color);
+            if (!pending) {
+                float *o = p.out + ((size_t)py * p.W + px) * 3;
+                o[0] = color.r;
+                o[1] = color.g;
+                o[2] = color.b;
+                busy = false;
+            }
+        }
+        // refill idle lanes: ballot + one atomic per wave + mbcnt prefix
+        if (!drained) {
+            unsigned long long idle = __ballot(!busy);
+            if (idle) {
+                unsigned n = (unsigned)__popcll(idle);
+                int leader = __ffsll((long long)idle) - 1;
+                unsigned base = 0;
+                if (lane == leader) base = atomicAdd(p.work, n);
+                base = __shfl(base, leader);
+                if (base + n >= p.total) drained = true;
+                if (!busy) {
+                    unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
+                    unsigned idx = base + rank;
+                    if (idx < p.total) {
+                        pixel_xy(p, idx, px, py);
+                        V3 pt = vadd(vadd(V3{p.ul[0], p.ul[1], p.ul[2]}, vmul(V3{p.dh[0], p.dh[1], p.dh[2]}, (float)px)),
+                                     vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)(py + p.y0)));
+                        V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
+                        q.o = eye;
+                        q.d = vnorm(vsub(pt, eye));
+                        q.tmin = 0.0f;               // primary rays accept any t > 0 (main.cpp:736)
+                        q.tmax = kFltMax;
+                        q.unb = false;
+                        q.self = -1;
+                        q.closest = true;
+                        q.skipchk = false;
+                        q.skipped = false;
+                        q.win = -1;
+                        ls.top = -1;
+                        cnt.prim++;
+                        busy = true;
+                        pending = true;
+                    }
+                }
+            }
+        }
+        if (!pending) q.tmin = kInf;                 // lane sits this scan out
+        if (__ballot(pending) == 0ull) break;
+        scan<SRC_LDS>(q, p, lds_f, lds_s);
+    }
+    unsigned long long *st = p.stats;
+    atomicAdd(&st[0], (unsigned long long)cnt.prim);
+    atomicAdd(&st[1], (unsigned long long)cnt.shadow);
+    atomicAdd(&st[2], (unsigned long long)cnt.refr);
+    atomicAdd(&st[3], (unsigned long long)cnt.refl);
+    atomicAdd(&st[4], (unsigned long long)cnt.skip);
+    atomicAdd(&st[5], (unsigned long long)cnt.ub);
+}
+
+}  // namespace rt
+
+// ===========================================================================
+// Host side: scene upload and the C ABI
+// ===========================================================================
+using namespace rt;
+
+struct rt_scene {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    Params base{};
+    std::vector<void *> allocs;
+    float *dev_out = nullptr;          // staging buffer when the caller passes host memory
+    size_t dev_out_bytes = 0;
+    unsigned int *work = nullptr;
+    unsigned long long *stats = nullptr;
+    int num_cu = 0;
+    size_t lds_bytes = 0;
+    long long opt_lds = -1;            // -1 auto, 0 off, 1 on
+    long long opt_grid = 0;            // blocks (0 = occupancy-derived)
+    hipStream_t last_stream = nullptr;
+    bool last_valid = false;
+};
+
+namespace {
+
+const char *kErr[] = {"ok", "invalid argument", "no such HIP device", "HIP runtime error", "out of device memory",
+                      "unsupported"};
+
+template <typename T, typename P>
+int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
+    size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
+    void *d = nullptr;
+    if (hipMalloc(&d, bytes) != hipSuccess) return RT_E_NOMEM;
+    s->allocs.push_back(d);
+    if (!v.empty() && hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+        return RT_E_HIP;
+    dst = static_cast<P>(d);
+    return RT_OK;
+}
+
+V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
+
+template <int MAXF, bool LDS>
+hipError_t launch_one(rt_scene *s, const Params &p, int grid, hipStream_t st) {
+    hipLaunchKernelGGL((render_kernel<MAXF, LDS>), dim3(grid), dim3(256), LDS ? s->lds_bytes : 0, st, p);
+    return hipGetLastError();
+}
+
+template <int MAXF>
+int occupancy(rt_scene *s, bool lds) {
+    int nb = 0;
+    if (lds)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, true>, 256, s->lds_bytes);
+    else
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, false>, 256, 0);
+    return nb;
+}
+
+int launch(rt_scene *s, Params &p, hipStream_t st) {
+    bool lds = s->opt_lds == 1 || (s->opt_lds == -1 && s->lds_bytes <= 64 * 1024);
+    if (s->lds_bytes > 160 * 1024) lds = false;
+    int depth = p.depth < 0 ? 0 : p.depth;
+    int nb;
+    if (depth <= 4) nb = occupancy<5>(s, lds);
+    else if (depth <= 8) nb = occupancy<9>(s, lds);
+    else if (depth <= 16) nb = occupancy<17>(s, lds);
+    else return RT_E_UNSUPPORTED;
+    if (nb < 1) nb = 1;
+    long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu;
+    long long need = ((long long)p.total + 255) / 256;
+    if (grid > need) grid = need;
+    if (grid < 1) grid = 1;
+    hipError_t e;
+    if (depth <= 4) e = lds ? launch_one<5, true>(s, p, (int)grid, st) : launch_one<5, false>(s, p, (int)grid, st);
+    else if (depth <= 8) e = lds ? launch_one<9, true>(s, p, (int)grid, st) : launch_one<9, false>(s, p, (int)grid, st);
+    else e = lds ? launch_one<17, true>(s, p, (int)grid, st) : launch_one<17, false>(s, p, (int)grid, st);
+    return e == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *rt_strerror(int code) {
+    int i = -code;
+    if (i < 0 || i > 5) return "unknown error";
+    return kErr[i];
+}
+
+int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
+    if (!desc || !out) return RT_E_INVALID;
+    *out = nullptr;
+    if (desc->n_spheres < 0 || desc->n_faces < 0 || desc->n_lights < 0 || desc->n_textures < 0) return RT_E_INVALID;
+    if ((desc->n_spheres && !desc->spheres) || (desc->n_faces && !desc->faces) ||
+        (desc->n_lights && !desc->lights) || (desc->n_textures && !desc->textures))
+        return RT_E_INVALID;
+    for (int i = 0; i < desc->n_spheres; i++)
+        if (desc->spheres[i].texture >= desc->n_textures) return RT_E_INVALID;
+    for (int i = 0; i < desc->n_faces; i++)
+        if (desc->faces[i].texture >= desc->n_textures) return RT_E_INVALID;
+    for (int i = 0; i < desc->n_textures; i++)
+        if (desc->textures[i].width <= 0 || desc->textures[i].height <= 0 || !desc->textures[i].rgb)
+            return RT_E_INVALID;
+    int ndev = rt_device_count();
+    if (device < 0 || device >= ndev) return RT_E_NODEVICE;
+    if (hipSetDevice(device) != hipSuccess) return RT_E_HIP;
+
+    auto *s = new rt_scene();
+    s->device = device;
+    const int nf = desc->n_faces, ns = desc->n_spheres, nobj = nf + ns;
+
+    // --- faces: exact per-face invariants (TraceRay recomputes these per call)
+    std::vector<float4> fscan((size_t)nf * 5);
+    std::vector<FaceShadeK> fsh((size_t)nf);
+    std::vector<ObjK> objs((size_t)nobj);
+    std::vector<float> ofac((size_t)nobj);
+    auto fill_obj = [&](int k, const rt_material &m, int tex, int is_sphere) {
+        ObjK &o = objs[k];
+        for (int c = 0; c < 3; c++) o.dif[c] = m.diffuse[c], o.spc[c] = m.specular[c];
+        o.ka = m.ka, o.kd = m.kd, o.ks = m.ks, o.n = m.n, o.opacity = m.opacity, o.eta = m.eta;
+        o.tex = tex;
+        o.is_sphere = is_sphere;
+        ofac[k] = (float)(1.0 - (double)m.opacity);
+    };
+    for (int i = 0; i < nf; i++) {
+        const rt_face_desc &F = desc->faces[i];
+        V3 v0 = f3(F.v[0]), v1 = f3(F.v[1]), v2 = f3(F.v[2]);
+        V3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
+        V3 n = vnorm(vcross(e1, e2));                         // main.cpp:537-539
+        float D = -vdot(n, v0);
+        float d11 = vdot(e1, e1), d12 = vdot(e1, e2), d22 = vdot(e2, e2);
+        float det = (d11 * d22 - d12 * d12);
+        fscan[5 * i + 0] = make_float4(v0.x, v0.y, v0.z, D);
+        fscan[5 * i + 1] = make_float4(n.x, n.y, n.z, det);
+        fscan[5 * i + 2] = make_float4(e1.x, e1.y, e1.z, d11);
+        fscan[5 * i + 3] = make_float4(e2.x, e2.y, e2.z, d22);
+        fscan[5 * i + 4] = make_float4(d12, 0.0f, 0.0f, 0.0f);
+        FaceShadeK &fs = fsh[i];
+        for (int k = 0; k < 3; k++) {
+            V3 vn = vnorm(f3(F.vn[k]));
+            fs.vn[k][0] = vn.x, fs.vn[k][1] = vn.y, fs.vn[k][2] = vn.z;
+            for (int c = 0; c < 2; c++) {
+                float t = F.vt[k][c];
+                fs.vt[k][c] = (t < 0.0f) ? 0.0f : ((1.0f < t) ? 1.0f : t);
+            }
+        }
+        fs.smooth = F.smooth;
+        fill_obj(i, F.mat, F.texture, 0);
+    }
+    std::vector<float4> sscan((size_t)ns);
+    for (int i = 0; i < ns; i++) {
+        const rt_sphere_desc &S = desc->spheres[i];
+        sscan[i] = make_float4(S.center[0], S.center[1], S.center[2], S.radius);
+        fill_obj(nf + i, S.mat, S.texture, 1);
+    }
+    std::vector<LightK> lights((size_t)desc->n_lights);
+    for (int i = 0; i < desc->n_lights; i++) {
+        const rt_light_desc &L = desc->lights[i];
+        LightK &k = lights[i];
+        memset(&k, 0, sizeof k);
+        for (int c = 0; c < 3; c++) k.xyz[c] = L.xyz[c], k.col[c] = L.color[c];
+        k.w = L.w;
+        V3 dir = f3(L.xyz);
+        V3 Ld = vmul(vnorm(dir), -1.0f);
+        V3 sd = vmul(dir, -1.0f);
+        k.L[0] = Ld.x, k.L[1] = Ld.y, k.L[2] = Ld.z;
+        k.sdir[0] = sd.x, k.sdir[1] = sd.y, k.sdir[2] = sd.z;
+    }
+    std::vector<TexK> texs((size_t)desc->n_textures);
+    std::vector<unsigned char> texels;
+    for (int i = 0; i < desc->n_textures; i++) {
+        const rt_texture_desc &T = desc->textures[i];
+        texs[i].w = T.width, texs[i].h = T.height, texs[i].off = (long long)texels.size();
+        texels.insert(texels.end(), T.rgb, T.rgb + (size_t)T.width * T.height * 3);
+    }
+
+    int rc = RT_OK;
+    Params &p = s->base;
+    if (!rc) rc = upload(s, fscan, p.fscan);
+    if (!rc) rc = upload(s, sscan, p.sscan);
+    if (!rc) rc = upload(s, ofac, p.ofac);
+    if (!rc) rc = upload(s, objs, p.objs);
+    if (!rc) rc = upload(s, fsh, p.fsh);
+    if (!rc) rc = upload(s, lights, p.lights);
+    if (!rc) rc = upload(s, texels, p.texels);
+    if (!rc) rc = upload(s, texs, p.texs);
+    if (!rc && hipMalloc(&s->work, sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
+    if (!rc && hipMalloc(&s->stats, 8 * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
+    if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
+    if (!rc && (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)) rc = RT_E_HIP;
+    if (!rc) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess) rc = RT_E_HIP;
+        else s->num_cu = prop.multiProcessorCount;
+    }
+    if (rc) {
+        rt_scene_destroy(s);
+        return rc;
+    }
+    p.nf = nf;
+    p.ns = ns;
+    p.nl = desc->n_lights;
+    for (int c = 0; c < 3; c++) p.bkg[c] = desc->bkg[c];
+    p.eta_bkg = desc->eta_bkg;
+    p.eps = desc->epsilon;
+    p.depth = desc->depth;
+    p.work = s->work;
+    p.stats = s->stats;
+    s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
+    *out = s;
+    return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene *s) {
+    if (!s) return RT_OK;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (void *d : s->allocs) (void)hipFree(d);
+    if (s->dev_out) (void)hipFree(s->dev_out);
+    if (s->work) (void)hipFree(s->work);
+    if (s->stats) (void)hipFree(s->stats);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+    return RT_OK;
+}
+
+int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
+    if (!s || !key) return RT_E_INVALID;
+    std::string k(key);
+    if (k == "lds") s->opt_lds = value;
+    else if (k == "grid") s->opt_grid = value;
+    else if (k == "depth") s->base.depth = (int)value;
+    else return RT_E_INVALID;
+    return RT_OK;
+}
+
+int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
+                         void *hip_stream) {
+    if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || y1 > H || y0 >= y1) return RT_E_INVALID;
+    if ((long long)W * (y1 - y0) >= (1ll << 31)) return RT_E_UNSUPPORTED;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : s->stream;
+    Params p = s->base;
+    for (int c = 0; c < 3; c++) {
+        p.eye[c] = cam->eye[c];
+        p.ul[c] = cam->ul[c];
+        p.dh[c] = cam->dh[c];
+        p.dv[c] = cam->dv[c];
+    }
+    p.W = W;
+    p.y0 = y0;
+    p.rows = y1 - y0;
+    p.total = (unsigned)((long long)W * (y1 - y0));
+    p.out = out_rgb;
+    if (hipMemsetAsync(s->work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
+    if (hipMemsetAsync(s->stats, 0, 8 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    (void)hipEventRecord(s->ev0, st);
+    int rc = launch(s, p, st);
+    (void)hipEventRecord(s->ev1, st);
+    s->last_stream = st;
+    s->last_valid = rc == RT_OK;
+    return rc;
+}
+
+int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
+    if (!s || !stats) return RT_E_INVALID;
+    if (!s->last_valid) return RT_E_INVALID;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
+    unsigned long long h[8];
+    if (hipMemcpy(h, s->stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    stats->primary = h[0];
+    stats->shadow = h[1];
+    stats->refraction = h[2];
+    stats->reflection = h[3];
+    stats->skip_trans = h[4];
+    stats->ub_back = h[5];
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, s->ev0, s->ev1);
+    stats->kernel_ms = ms;
+    return RT_OK;
+}
+
+int rt_render_rows(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb, rt_stats *stats) {
+    if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || y1 > H || y0 >= y1) return RT_E_INVALID;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    hipPointerAttribute_t attr;
+    bool on_device = false;
+    if (hipPointerGetAttributes(&attr, out_rgb) == hipSuccess)
+        on_device = attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+    else
+        (void)hipGetLastError();
+    size_t bytes = (size_t)W * (size_t)(y1 - y0) * 3 * sizeof(float);
+    float *dst = out_rgb;
+    if (!on_device) {
+        if (s->dev_out_bytes < bytes) {
+            if (s->dev_out) (void)hipFree(s->dev_out);
+            s->dev_out = nullptr;
+            s->dev_out_bytes = 0;
+            if (hipMalloc(&s->dev_out, bytes) != hipSuccess) return RT_E_NOMEM;
+            s->dev_out_bytes = bytes;
+        }
+        dst = s->dev_out;
+    }
+    int rc = rt_render_rows_async(s, cam, W, H, y0, y1, dst, nullptr);
+    if (rc) return rc;
+    if (!on_device && hipMemcpyAsync(out_rgb, dst, bytes, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+        return RT_E_HIP;
+    if (hipStreamSynchronize(s->stream) != hipSuccess) return RT_E_HIP;
+    if (stats) return rt_scene_last_stats(s, stats);
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,303 @@
+"""ctypes bindings for the MI355X renderer's two C ABIs.
+
+  librt_host.so  include/rt_host.h  scene parser, camera, quantiser, PPM writer
+  librt_hip.so   include/rt_hip.h   gfx950 kernels (the hot path)
+
+Mirrors the reference's single entry point
+``create_view_window_and_ray_trace`` (main.cpp:670) as :func:`render_scene`
+and its ``main`` (main.cpp:60-657) as :func:`render_file`.  There is no CPU
+fallback: when the HIP library or a device is missing these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+
+RT_OK = 0
+ERRORS = {-1: "invalid argument", -2: "no such HIP device", -3: "HIP runtime error",
+          -4: "out of device memory", -5: "unsupported"}
+
+
+class RTError(RuntimeError):
+    pass
+
+
+class rt_material(C.Structure):
+    _fields_ = [("diffuse", C.c_float * 3), ("specular", C.c_float * 3), ("ka", C.c_float),
+                ("kd", C.c_float), ("ks", C.c_float), ("n", C.c_float), ("opacity", C.c_float),
+                ("eta", C.c_float)]
+
+
+class rt_sphere_desc(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("radius", C.c_float), ("mat", rt_material),
+                ("texture", C.c_int)]
+
+
+class rt_face_desc(C.Structure):
+    _fields_ = [("v", (C.c_float * 3) * 3), ("vn", (C.c_float * 3) * 3), ("vt", (C.c_float * 2) * 3),
+                ("smooth", C.c_int), ("mat", rt_material), ("texture", C.c_int)]
+
+
+class rt_light_desc(C.Structure):
+    _fields_ = [("xyz", C.c_float * 3), ("w", C.c_float), ("color", C.c_float * 3)]
+
+
+class rt_texture_desc(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("rgb", C.POINTER(C.c_ubyte))]
+
+
+class rt_scene_desc(C.Structure):
+    _fields_ = [("n_spheres", C.c_int), ("spheres", C.POINTER(rt_sphere_desc)),
+                ("n_faces", C.c_int), ("faces", C.POINTER(rt_face_desc)),
+                ("n_lights", C.c_int), ("lights", C.POINTER(rt_light_desc)),
+                ("n_textures", C.c_int), ("textures", C.POINTER(rt_texture_desc)),
+                ("bkg", C.c_float * 3), ("eta_bkg", C.c_float), ("epsilon", C.c_float),
+                ("depth", C.c_int)]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("ul", C.c_float * 3), ("dh", C.c_float * 3),
+                ("dv", C.c_float * 3)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("primary", C.c_ulonglong), ("shadow", C.c_ulonglong),
+                ("refraction", C.c_ulonglong), ("reflection", C.c_ulonglong),
+                ("skip_trans", C.c_ulonglong), ("ub_back", C.c_ulonglong),
+                ("kernel_ms", C.c_double)]
+
+    def rays(self) -> int:
+        return int(self.primary + self.shadow + self.refraction + self.reflection)
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_host = None
+_hip = None
+
+HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_set_imsize",
+                "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
+                "rth_output_path"]
+HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
+               "rt_render_rows_async", "rt_scene_last_stats", "rt_scene_set_option", "rt_strerror"]
+
+
+def host_lib() -> C.CDLL:
+    global _host
+    if _host is None:
+        path = os.path.join(LIB_DIR, "librt_host.so")
+        if not os.path.exists(path):
+            raise RTError(f"{path} missing: run `make -C simple-raytracer_amd` (or __graft_entry__.build())")
+        L = C.CDLL(path)
+        L.rth_parse_file.argtypes = [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
+        L.rth_free.argtypes = [C.c_void_p]
+        L.rth_desc.argtypes = [C.c_void_p]
+        L.rth_desc.restype = C.POINTER(rt_scene_desc)
+        L.rth_set_depth.argtypes = [C.c_void_p, C.c_int]
+        L.rth_set_imsize.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.rth_width.argtypes = [C.c_void_p]
+        L.rth_height.argtypes = [C.c_void_p]
+        L.rth_camera.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_camera)]
+        L.rth_quantize.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
+        L.rth_write_ppm.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.rth_output_path.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        _host = L
+    return _host
+
+
+def hip_lib() -> C.CDLL:
+    """The HIP layer.  Raises (never falls back) when it is missing."""
+    global _hip
+    if _hip is None:
+        path = os.path.join(LIB_DIR, "librt_hip.so")
+        if not os.path.exists(path):
+            raise RTError(f"{path} missing: the HIP path is required (no CPU fallback)")
+        L = C.CDLL(path)
+        L.rt_device_count.restype = C.c_int
+        L.rt_scene_create.argtypes = [C.c_int, C.POINTER(rt_scene_desc), C.POINTER(C.c_void_p)]
+        L.rt_scene_destroy.argtypes = [C.c_void_p]
+        L.rt_render_rows.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
+                                     C.c_int, C.c_void_p, C.POINTER(rt_stats)]
+        L.rt_render_rows_async.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int,
+                                           C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
+        L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
+        L.rt_strerror.argtypes = [C.c_int]
+        L.rt_strerror.restype = C.c_char_p
+        _hip = L
+    return _hip
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != RT_OK:
+        raise RTError(f"{what}: {ERRORS.get(rc, rc)} ({rc})")
+
+
+class ParseError(RTError):
+    """The reference would abort (uncaught exception).  .lines = its std::cerr output."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+        self.lines = msg.split("\n")
+
+
+class MissingCommand(RTError):
+    """The reference would print .message on stdout and exit 0 without an image."""
+
+
+class HostScene:
+    """A parsed scene file (main.cpp:88-602).  Texture paths resolve against
+    the current directory, or against `cwd` when given."""
+
+    def __init__(self, path: str, cwd: str | None = None):
+        L = host_lib()
+        h = C.c_void_p()
+        buf = C.create_string_buffer(1 << 16)
+        old = os.getcwd()
+        try:
+            if cwd:
+                os.chdir(cwd)
+            rc = L.rth_parse_file(os.fsencode(path), C.byref(h), buf, len(buf))
+        finally:
+            os.chdir(old)
+        msg = buf.value.decode(errors="replace")
+        if rc > 0:
+            raise MissingCommand(msg)
+        if rc < 0:
+            raise ParseError(rc, msg)
+        self._h = h
+        self.path = path
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            host_lib().rth_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def desc(self) -> rt_scene_desc:
+        return host_lib().rth_desc(self._h).contents
+
+    def set_depth(self, depth: int) -> None:
+        host_lib().rth_set_depth(self._h, depth)
+
+    def set_imsize(self, w: int, h: int) -> None:
+        host_lib().rth_set_imsize(self._h, w, h)
+
+    @property
+    def width(self) -> int:
+        return host_lib().rth_width(self._h)
+
+    @property
+    def height(self) -> int:
+        return host_lib().rth_height(self._h)
+
+    def camera(self, W: int | None = None, H: int | None = None) -> rt_camera:
+        cam = rt_camera()
+        _check(host_lib().rth_camera(self._h, W or self.width, H or self.height, C.byref(cam)),
+               "rth_camera")
+        return cam
+
+
+def quantize(rgb: np.ndarray) -> np.ndarray:
+    """main.cpp:760-762: the reference's size_t pixel values (as int64)."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    out = np.empty(a.shape, dtype=np.int64)
+    host_lib().rth_quantize(a.ctypes.data, a.size, out.ctypes.data)
+    return out
+
+
+def write_ppm(path: str, rgb: np.ndarray, threads: int = 0) -> None:
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    H, W = a.shape[:2]
+    if host_lib().rth_write_ppm(os.fsencode(path), a.ctypes.data, W, H, threads) != 0:
+        raise RTError(f"cannot write {path}")
+
+
+def output_path(scene_path: str) -> str:
+    buf = C.create_string_buffer(4096)
+    host_lib().rth_output_path(os.fsencode(scene_path), buf, len(buf))
+    return buf.value.decode()
+
+
+def device_count() -> int:
+    return hip_lib().rt_device_count()
+
+
+class GpuScene:
+    """A scene uploaded to one HIP device (rt_scene_create)."""
+
+    def __init__(self, host: HostScene, device: int = 0):
+        L = hip_lib()
+        h = C.c_void_p()
+        _check(L.rt_scene_create(device, host.desc, C.byref(h)), "rt_scene_create")
+        self._h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            hip_lib().rt_scene_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(hip_lib().rt_scene_set_option(self._h, key.encode(), int(value)), "rt_scene_set_option")
+
+    def render_rows(self, cam: rt_camera, W: int, H: int, y0: int, y1: int, out=None):
+        """Synchronous render of rows [y0, y1).  `out` may be a numpy array
+        (host) or an int device pointer; returns (out, rt_stats)."""
+        st = rt_stats()
+        if out is None:
+            out = np.empty((y1 - y0, W, 3), dtype=np.float32)
+        ptr = out if isinstance(out, int) else out.ctypes.data
+        _check(hip_lib().rt_render_rows(self._h, C.byref(cam), W, H, y0, y1, C.c_void_p(ptr),
+                                        C.byref(st)), "rt_render_rows")
+        return out, st
+
+    def render_rows_async(self, cam: rt_camera, W: int, H: int, y0: int, y1: int, dev_ptr: int,
+                          stream: int | None = None) -> None:
+        _check(hip_lib().rt_render_rows_async(self._h, C.byref(cam), W, H, y0, y1,
+                                              C.c_void_p(dev_ptr), C.c_void_p(stream or 0)),
+               "rt_render_rows_async")
+
+    def last_stats(self) -> rt_stats:
+        st = rt_stats()
+        _check(hip_lib().rt_scene_last_stats(self._h, C.byref(st)), "rt_scene_last_stats")
+        return st
+
+
+def render_scene(path: str, cwd: str | None = None, device: int = 0, depth: int | None = None,
+                 imsize: tuple[int, int] | None = None, rows: tuple[int, int] | None = None):
+    """Parse + render a scene file on the GPU: returns (float32 HxWx3, rt_stats)."""
+    hs = HostScene(path, cwd=cwd)
+    if depth is not None:
+        hs.set_depth(depth)
+    if imsize is not None:
+        hs.set_imsize(*imsize)
+    W, H = hs.width, hs.height
+    cam = hs.camera(W, H)
+    y0, y1 = rows if rows else (0, H)
+    gs = GpuScene(hs, device)
+    try:
+        img, st = gs.render_rows(cam, W, H, y0, y1)
+    finally:
+        gs.close()
+        hs.close()
+    return img, st
+
+
+def render_file(path: str, device: int = 0) -> str:
+    """The reference's main(): render `path` and write <stem>.ppm; returns it."""
+    img, _ = render_scene(path, device=device)
+    out = output_path(path)
+    write_ppm(out, img)
+    return out

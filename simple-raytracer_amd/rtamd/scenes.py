@@ -1,0 +1,135 @@
+"""Seeded synthetic scene + texture generators for the benchmark configs.
+
+The scene *text file* is the artifact: it is parsed by the
+same front end as any reference scene (main.cpp:88-602 keyword set).
+
+Configs (BASELINE.json "configs"):
+  C1  Examples/basic_geometry_tests/* at imsize 256x256      (CPU plumbing)
+  C2  1024^2, 100 spheres, 2 point lights, ks=0
+  C3  4096^2, 1000 spheres + 1000 triangles, ks=0.5, 10% glass, depth 4
+  C4  8192^2, 10k textured triangles + 1 directional + 1 point light
+  C5  16384^2, 100k spheres, reflection + refraction, depth 8
+"""
+from __future__ import annotations
+
+import os
+import random
+
+import numpy as np
+
+HEADER = (
+    "eye 0 0 0\n"
+    "viewdir 0 0 -1\n"
+    "updir 0 1 0\n"
+    "hfov 60\n"
+    "imsize {w} {h}\n"
+    "bkgcolor 0.1 0.1 0.1 1\n"
+)
+
+CONFIGS = {
+    "C2": dict(w=1024, h=1024, spheres=100, tris=0, ks=0.0, glass=0.0, textured=False,
+               lights="point2", depth=4),
+    "C3": dict(w=4096, h=4096, spheres=1000, tris=1000, ks=0.5, glass=0.10, textured=False,
+               lights="point2", depth=4),
+    "C4": dict(w=8192, h=8192, spheres=0, tris=10000, ks=0.0, glass=0.0, textured=True,
+               lights="dir+point", depth=4),
+    "C5": dict(w=16384, h=16384, spheres=100000, tris=0, ks=0.5, glass=0.10, textured=False,
+               lights="point2", depth=8),
+}
+
+TEXTURE_NAME = "c4_texture.ppm"
+
+
+def _f(x: float) -> str:
+    return f"{x:.6f}"
+
+
+def scene_text(name: str, w: int | None = None, h: int | None = None, seed: int = 1234,
+               n_spheres: int | None = None, n_tris: int | None = None) -> str:
+    """Return the scene file text for config `name` (optionally resized)."""
+    cfg = dict(CONFIGS[name])
+    if w is not None:
+        cfg["w"], cfg["h"] = w, h
+    if n_spheres is not None:
+        cfg["spheres"] = n_spheres
+    if n_tris is not None:
+        cfg["tris"] = n_tris
+    rnd = random.Random(seed)
+    out = [HEADER.format(w=cfg["w"], h=cfg["h"])]
+    if cfg["lights"] == "point2":
+        out.append("light -10 10 0 1 0.6 0.6 0.6\n")
+        out.append("light 10 8 -10 1 0.6 0.6 0.6\n")
+    else:
+        out.append("light 1 -1 -1 0 0.6 0.6 0.6\n")
+        out.append("light -10 10 0 1 0.6 0.6 0.6\n")
+    ks = cfg["ks"]
+
+    def mtl(glass: bool) -> str:
+        r, g, b = rnd.random(), rnd.random(), rnd.random()
+        s = f"mtlcolor {_f(r)} {_f(g)} {_f(b)} 1 1 1 0.2 0.6 {_f(ks)} 20"
+        if glass:
+            s += " 0.3 1.5"
+        return s + "\n"
+
+    def centre():
+        return (rnd.uniform(-20, 20), rnd.uniform(-20, 20), rnd.uniform(-60, -20))
+
+    # triangles first in the file (ids are a shared counter; the reference
+    # visits all faces before all spheres regardless, main.cpp:1218)
+    nt = cfg["tris"]
+    if nt:
+        if cfg["textured"]:
+            out.append(mtl(False))
+            out.append(f"texture {TEXTURE_NAME}\n")
+        for i in range(nt):
+            cx, cy, cz = centre()
+            for _ in range(3):
+                out.append("v {} {} {}\n".format(_f(cx + rnd.uniform(-1.5, 1.5)),
+                                                  _f(cy + rnd.uniform(-1.5, 1.5)),
+                                                  _f(cz + rnd.uniform(-1.5, 1.5))))
+            if cfg["textured"]:
+                for _ in range(3):
+                    out.append(f"vt {_f(rnd.random())} {_f(rnd.random())}\n")
+                b = 3 * i
+                out.append(f"f {b+1}/{b+1} {b+2}/{b+2} {b+3}/{b+3}\n")
+            else:
+                out.append(mtl(False))
+                b = 3 * i
+                out.append(f"f {b+1} {b+2} {b+3}\n")
+    for i in range(cfg["spheres"]):
+        glass = rnd.random() < cfg["glass"]
+        out.append(mtl(glass))
+        cx, cy, cz = centre()
+        out.append(f"sphere {_f(cx)} {_f(cy)} {_f(cz)} {_f(rnd.uniform(0.3, 1.2))}\n")
+    return "".join(out)
+
+
+def texture_p3(w: int, h: int, seed: int = 7) -> str:
+    """Deterministic synthetic P3 texture (the real textures are LFS stubs)."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    r = (x * 255 // max(w - 1, 1)).astype(np.int64)
+    g = (y * 255 // max(h - 1, 1)).astype(np.int64)
+    b = (((x // 8 + y // 8) % 2) * 180 + rng.integers(0, 75, size=(h, w))).astype(np.int64)
+    img = np.stack([r, g, b], axis=-1).clip(0, 255)
+    lines = ["P3", f"{w} {h}", "255"]
+    for row in img:
+        lines.append(" ".join(str(int(v)) for v in row.reshape(-1)))
+    return "\n".join(lines) + "\n"
+
+
+def write_scene(dirpath: str, name: str, **kw) -> str:
+    """Write config `name` to dirpath/<name>.txt (+ texture) and return the path."""
+    os.makedirs(dirpath, exist_ok=True)
+    tag = kw.pop("tag", name)
+    path = os.path.join(dirpath, f"{tag}.txt")
+    txt = scene_text(name, **kw)
+    if not (os.path.exists(path) and open(path).read() == txt):
+        with open(path, "w") as f:
+            f.write(txt)
+    if CONFIGS[name]["textured"]:
+        tp = os.path.join(dirpath, TEXTURE_NAME)
+        if not os.path.exists(tp):
+            with open(tp, "w") as f:
+                f.write(texture_p3(2048, 1024))
+    return path
