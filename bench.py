@@ -47,7 +47,7 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
-    ap.add_argument("--cpu-sample", type=int, default=128,
+    ap.add_argument("--cpu-sample", type=int, default=256,
                     help="cpu_baseline: the reference renders the same scene at NxN")
     ap.add_argument("--option", action="append", default=[],
                     help="kernel option key=value (rt_scene_set_option)")
@@ -134,14 +134,12 @@ def main() -> None:
         gs.set_option(k, int(v))
 
     # strong scaling: contiguous row strips, equal counts for the gather
-    rows_per = (H + world - 1) // world
-    y0 = min(H, rank * rows_per)
-    y1 = min(H, y0 + rows_per)
-    strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device="cuda")
-    gather_list = None
-    if world > 1 and rank == 0:
-        gather_list = [torch.empty_like(strip) for _ in range(world)]
-    stream = torch.cuda.current_stream()
+    from rtamd.dist import alloc_strips, gather_strips, strip_rows
+    y0, y1, _ = strip_rows(H, world, rank)
+    strip, gather_list = alloc_strips(H, W, world, rank, "cuda", torch)
+    # a dedicated (non-null) stream: the render kernel, its timing events and
+    # the RCCL gather are all ordered on it
+    stream = torch.cuda.Stream()
 
     def step(ev=None):
         if ev is not None:
@@ -151,8 +149,9 @@ def main() -> None:
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            dist.gather(strip, gather_list, dst=0)
+            gather_strips(strip, gather_list, world, rank, H, dist, torch)
 
+    torch.cuda.set_stream(stream)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

@@ -72,6 +72,22 @@ constexpr float kFltMax = 3.40282347e+38f;            // std::numeric_limits<flo
 
 enum { ENTERING = 0, EXITING = 1 };
 
+// Read-only scene data seen through the constant address space: the loads
+// are wave-uniform and invariant, so they become scalar (s_load) reads into
+// SGPRs through the scalar cache instead of 64 identical per-lane loads.
+#define RT_CONST __attribute__((address_space(4)))
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ const RT_CONST T *cst(const T *p) {
+    return (const RT_CONST T *)p;
+}
+// uniform float4 read via the scalar unit
+__device__ __forceinline__ float4 sld4(const float4 *p, int i) {
+    f4v v = cst((const f4v *)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+
 // ---------------------------------------------------------------------------
 // Device scene layout (built by rt_scene_create)
 // ---------------------------------------------------------------------------
@@ -157,7 +173,7 @@ __device__ __forceinline__ void offer(Query &q, float t, int obj, const float *_
                 q.win = obj;
             }
         } else {
-            float f = ofac[obj];
+            float f = cst(ofac)[obj];
             q.mask = cmulf(q.mask, f);
             // an opaque occluder zeroes the mask for good: any-hit termination
             if ((q.mask.r == 0.0f) & (q.mask.g == 0.0f) & (q.mask.b == 0.0f)) q.tmin = kInf;
@@ -198,13 +214,18 @@ __device__ __forceinline__ bool sphere_test(float4 s, V3 o, V3 d, float &t1, flo
 }
 
 // The scan every active lane of the wave runs together.  SRC_LDS: primitive
-// arrays were staged into LDS (lds_f, lds_s); otherwise global (scalar) loads.
+// arrays were staged into LDS (lds_f, lds_s); otherwise scalar loads.
 template <bool SRC_LDS>
 __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s) {
-    const float4 *F = SRC_LDS ? lds_f : p.fscan;
-    const float4 *S = SRC_LDS ? lds_s : p.sscan;
     for (int i = 0; i < p.nf; i++) {
-        float4 f0 = F[5 * i + 0], f1 = F[5 * i + 1], f2 = F[5 * i + 2], f3 = F[5 * i + 3], f4 = F[5 * i + 4];
+        float4 f0, f1, f2, f3, f4;
+        if (SRC_LDS) {
+            f0 = lds_f[5 * i + 0], f1 = lds_f[5 * i + 1], f2 = lds_f[5 * i + 2], f3 = lds_f[5 * i + 3];
+            f4 = lds_f[5 * i + 4];
+        } else {
+            f0 = sld4(p.fscan, 5 * i + 0), f1 = sld4(p.fscan, 5 * i + 1), f2 = sld4(p.fscan, 5 * i + 2);
+            f3 = sld4(p.fscan, 5 * i + 3), f4 = sld4(p.fscan, 5 * i + 4);
+        }
         if (f1.w == 0.0f) continue;                 // det == 0: never intersects (main.cpp:1367)
         if (q.tmin < kInf) {
             float t, a, b, g;
@@ -212,7 +233,7 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
         }
     }
     for (int i = 0; i < p.ns; i++) {
-        float4 s = S[i];
+        float4 s = SRC_LDS ? lds_s[i] : sld4(p.sscan, i);
         if (q.tmin < kInf) {
             float t1, t2;
             if (sphere_test(s, q.o, q.d, t1, t2)) {

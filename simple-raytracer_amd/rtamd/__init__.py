@@ -118,6 +118,14 @@ def hip_lib() -> C.CDLL:
         path = os.path.join(LIB_DIR, "librt_hip.so")
         if not os.path.exists(path):
             raise RTError(f"{path} missing: the HIP path is required (no CPU fallback)")
+        # One HIP runtime per process: torch ships its own libamdhip64.so with
+        # the same soname as /opt/rocm's.  Whichever is loaded first serves
+        # both; loading ours first leaves torch without devices, so let torch
+        # load its runtime first when it is installed.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(path)
         L.rt_device_count.restype = C.c_int
         L.rt_scene_create.argtypes = [C.c_int, C.POINTER(rt_scene_desc), C.POINTER(C.c_void_p)]

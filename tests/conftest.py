@@ -31,8 +31,29 @@ def _ensure_built():
                        stdout=subprocess.DEVNULL)
 
 
+def _ensure_generated_scenes():
+    """Seeded synthetic fixture scenes are regenerated (not committed: C5's
+    is 10 MB) and must reproduce the exact text the goldens were made from."""
+    import hashlib
+    from rtamd import scenes as gen
+    with open(os.path.join(GOLD_DIR, "golden.json")) as f:
+        g = json.load(f)
+    for name, ent in g.items():
+        spec = ent.get("generated")
+        if not spec:
+            continue
+        path = os.path.join(SCENES, name)
+        if not os.path.exists(path):
+            txt = gen.scene_text(spec["config"], w=spec["w"], h=spec["h"])
+            with open(path, "w") as f:
+                f.write(txt)
+        with open(path, "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == spec["sha256"], f"generator drift: {name}"
+
+
 def pytest_sessionstart(session):
     _ensure_built()
+    _ensure_generated_scenes()
 
 
 @pytest.fixture(scope="session")

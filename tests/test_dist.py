@@ -1,0 +1,71 @@
+"""Multi-rank sharding + gather (bench.py's N>1 data path) on CPU with gloo.
+
+Each rank renders its row strip -- here with the CPU oracle standing in for
+the GPU renderer, since this test runs without a GPU -- and rank 0 must
+reassemble exactly the full-image render."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import SCENES
+from rtamd.dist import alloc_strips, gather_strips, strip_rows
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, scene, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle_py import OracleScene
+    sc = OracleScene(scene, cwd=SCENES)
+    W, H = sc.width, sc.height
+    y0, y1, rows_per = strip_rows(H, world, rank)
+    strip, targets = alloc_strips(H, W, world, rank, "cpu", torch)
+    if y1 > y0:
+        img, _ = sc.render(rows=np.arange(y0, y1))
+        strip[: y1 - y0] = torch.from_numpy(img)
+    full = gather_strips(strip, targets, world, rank, H, dist, torch)
+    if rank == 0:
+        out_q.put(full.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_reassembles_image(world):
+    scene = "test7_s.txt"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scene, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from oracle_py import OracleScene
+    ref, _ = OracleScene(scene, cwd=SCENES).render()
+    assert np.array_equal(np.nan_to_num(full, nan=-9), np.nan_to_num(ref, nan=-9))
+
+
+def test_strip_rows_cover_image():
+    for H in (1, 7, 64, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            rows = []
+            for r in range(world):
+                y0, y1, per = strip_rows(H, world, r)
+                assert 0 <= y1 - y0 <= per
+                rows += list(range(y0, y1))
+            assert rows == list(range(H))

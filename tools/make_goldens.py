@@ -140,6 +140,7 @@ def main() -> None:
         open(os.path.join(SCN, base + "_256.txt"), "w").write(set_imsize(txt, 256, 256))
         scenes.append(base + "_256.txt")
     # seeded synthetic miniatures of C2-C5 (reference depth is fixed at 4)
+    generated = {}
     minis = {"C2": (128, 128, {}), "C3": (64, 64, {}), "C4": (32, 32, {}),
              "C5": (8, 8, {})}
     for cname, (w, h, kw) in minis.items():
@@ -147,6 +148,8 @@ def main() -> None:
         fn = f"{cname}_{w}x{h}.txt"
         open(os.path.join(SCN, fn), "w").write(txt)
         scenes.append(fn)
+        generated[fn] = {"config": cname, "w": w, "h": h,
+                         "sha256": hashlib.sha256(txt.encode()).hexdigest()}
     # edge-case scenes (hand-written, already in SCN)
     scenes += sorted(f for f in os.listdir(SCN) if f.startswith("edge_") and f.endswith(".txt"))
 
@@ -160,6 +163,8 @@ def main() -> None:
         h, w, _ = q.shape
         ent = dict(scene=fn, width=w, height=h, md5=md5, trace_calls=trace, shade_calls=shade,
                    nan_px=int((q == -2**31).any(axis=2).sum()))
+        if fn in generated:
+            ent["generated"] = generated[fn]
         if w * h <= NPZ_MAX_PX:
             np.savez_compressed(os.path.join(GOLD, "ref_q", fn[:-4] + ".npz"), q=q)
             ent["npz"] = "ref_q/" + fn[:-4] + ".npz"
