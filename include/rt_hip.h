@@ -123,6 +123,9 @@ typedef struct {
     unsigned long long skip_trans;   /* 'goto SKIP_TRANS' taken (main.cpp:1001) */
     unsigned long long ub_back;      /* back() on an empty medium stack (main.cpp:1028, UB in the reference) */
     double kernel_ms;                /* device time of the render kernel(s) */
+    unsigned long long box_tests;    /* ray-box tests executed (BVH traversal) */
+    unsigned long long face_tests;   /* ray-triangle tests executed */
+    unsigned long long sphere_tests; /* ray-sphere tests executed */
 } rt_stats;
 
 typedef struct rt_scene rt_scene;
@@ -146,7 +149,9 @@ int rt_render_rows_async(rt_scene *scene, const rt_camera *cam, int W, int H, in
                          void *hip_stream);
 int rt_scene_last_stats(rt_scene *scene, rt_stats *stats);
 
-/* Kernel selection / tuning knobs (0 = automatic). */
+/* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
+ * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
+ * (persistent blocks, 0 = occupancy), "depth" (recursion depth override). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
 const char *rt_strerror(int code);

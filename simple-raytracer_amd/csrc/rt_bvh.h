@@ -1,0 +1,207 @@
+// rt_bvh.h -- host-side BVH builder for the MI355X renderer (header-only,
+// included by rt_kernels.hip's host code).
+//
+// The reference scans every primitive for every ray (TraceRay, main.cpp:1218-
+// 1403).  The BVH only decides WHICH primitives a ray can possibly hit; every
+// candidate is still tested with the reference's exact formulas, and the
+// device traversal reproduces the reference's visiting order where it matters
+// (closest-hit ties, shadow-mask product order).  For that the
+// boxes must be conservative for the *computed* intersections, which deviate
+// from exact geometry by rounding:
+//   face:   the accepted hit point is within a few ulp(scene scale) of the
+//           triangle -> pad by 2^-14 * D * cond(triangle), cond = |e1|^2|e2|^2/det
+//   sphere: the discriminant B^2 - 4C is computed with absolute error up to
+//           ~2^-18.4 D^2 (|dir| <= D), so rays up to sqrt(r^2 + 2^-18 D^2) from
+//           the centre can be "hits" -> radius grown accordingly
+// where D bounds the distance from any ray origin (eye or a surface point) to
+// any primitive.  (The directional-light sphere quirk -- A = 1 assumed for an
+// unnormalised direction -- is not geometric at all; those rays bypass the BVH.)
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+namespace rtbvh {
+
+struct Box {
+    float lo[3] = {INFINITY, INFINITY, INFINITY};
+    float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const Box &b) {
+        for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], b.lo[k]), hi[k] = std::max(hi[k], b.hi[k]);
+    }
+    void grow(const float p[3]) {
+        for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], p[k]), hi[k] = std::max(hi[k], p[k]);
+    }
+    float area() const {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0f;
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+// 64-byte node: both children's boxes + child links.  link >= 0: inner node
+// index; link < 0: leaf, -(1 + (first << 4 | count)), count <= 15.
+struct Node {
+    float l_lo[3], l_hi0;
+    float l_hi12[2], r_lo01[2];
+    float r_lo2, r_hi[3];
+    int32_t link[2];
+    int32_t pad[2];
+};
+static_assert(sizeof(Node) == 64, "node layout");
+
+struct Prim {
+    Box box;
+    float c[3];
+    float cost;   // relative intersection cost
+    int key;      // object index (reference visiting order)
+};
+
+struct Result {
+    std::vector<Node> nodes;
+    std::vector<int32_t> keys;   // leaf-ordered object indices
+    int depth = 0;
+};
+
+inline int32_t leaf_link(int first, int count) { return -(1 + ((first << 4) | count)); }
+
+class Builder {
+   public:
+    static constexpr int kBins = 32;
+    static constexpr int kMaxLeaf = 8;      // SAH leaves (<= 15 fits the link encoding)
+    static constexpr int kSahDepth = 22;    // deeper: object-median splits (bounded depth)
+    static constexpr int kMaxDepth = 40;    // the device traversal stack holds 40 entries
+
+    explicit Builder(std::vector<Prim> &prims) : P(prims) {}
+
+    // Returns false if the tree would be deeper than kMaxDepth.
+    bool build(Result &R) {
+        out = &R;
+        R = Result();
+        if (P.empty()) return true;
+        idx.resize(P.size());
+        for (size_t i = 0; i < P.size(); i++) idx[i] = (int)i;
+        R.nodes.reserve(P.size());
+        R.nodes.emplace_back();                       // the root is node 0
+        int mid = split_point(0, (int)P.size(), 1);
+        if (mid < 0) mid = (int)P.size();             // everything in one leaf
+        int32_t l = mid > 0 ? build_range(0, mid, 2) : leaf_link(0, 0);
+        int32_t r = mid < (int)P.size() ? build_range(mid, (int)P.size(), 2) : leaf_link(0, 0);
+        set_child(R.nodes[0], 0, bounds(0, mid), l);
+        set_child(R.nodes[0], 1, bounds(mid, (int)P.size()), r);
+        R.depth = std::max(R.depth, 1);
+        R.keys.resize(P.size());
+        for (size_t i = 0; i < P.size(); i++) R.keys[i] = P[idx[i]].key;
+        return R.depth <= kMaxDepth;
+    }
+
+   private:
+    std::vector<Prim> &P;
+    std::vector<int> idx;
+    Result *out = nullptr;
+
+    static void set_child(Node &n, int side, const Box &b, int32_t link) {
+        if (side == 0) {
+            n.l_lo[0] = b.lo[0], n.l_lo[1] = b.lo[1], n.l_lo[2] = b.lo[2];
+            n.l_hi0 = b.hi[0], n.l_hi12[0] = b.hi[1], n.l_hi12[1] = b.hi[2];
+        } else {
+            n.r_lo01[0] = b.lo[0], n.r_lo01[1] = b.lo[1], n.r_lo2 = b.lo[2];
+            n.r_hi[0] = b.hi[0], n.r_hi[1] = b.hi[1], n.r_hi[2] = b.hi[2];
+        }
+        n.link[side] = link;
+    }
+
+    Box bounds(int a, int b) const {
+        Box x;
+        for (int i = a; i < b; i++) x.grow(P[idx[i]].box);
+        return x;
+    }
+
+    // Partition [a, b) and return the split position, or -1 for "make a leaf".
+    int split_point(int a, int b, int depth) {
+        int n = b - a;
+        if (n <= 1) return -1;
+        Box cb;
+        float cost_leaf = 0;
+        for (int i = a; i < b; i++) {
+            cb.grow(P[idx[i]].c);
+            cost_leaf += P[idx[i]].cost;
+        }
+        if (depth > kSahDepth) {
+            if (n <= 2) return -1;
+            int ax = 0;
+            for (int k = 1; k < 3; k++)
+                if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+            int mid = a + n / 2;
+            std::nth_element(idx.begin() + a, idx.begin() + mid, idx.begin() + b,
+                             [&](int x, int y) { return P[x].c[ax] < P[y].c[ax]; });
+            return mid;
+        }
+        float best = INFINITY;
+        int best_axis = -1, best_bin = -1;
+        for (int ax = 0; ax < 3; ax++) {
+            float lo = cb.lo[ax], hi = cb.hi[ax];
+            if (!(hi > lo)) continue;
+            float scale = kBins / (hi - lo);
+            Box bb[kBins];
+            float cc[kBins] = {0};
+            for (int i = a; i < b; i++) {
+                const Prim &p = P[idx[i]];
+                int k = std::min(kBins - 1, std::max(0, (int)((p.c[ax] - lo) * scale)));
+                bb[k].grow(p.box);
+                cc[k] += p.cost;
+            }
+            Box left[kBins];
+            float lc[kBins];
+            Box acc;
+            float c = 0;
+            for (int k = 0; k < kBins; k++) {
+                acc.grow(bb[k]);
+                c += cc[k];
+                left[k] = acc;
+                lc[k] = c;
+            }
+            acc = Box();
+            c = 0;
+            for (int k = kBins - 1; k > 0; k--) {
+                acc.grow(bb[k]);
+                c += cc[k];
+                if (lc[k - 1] == 0 || c == 0) continue;
+                float s = left[k - 1].area() * lc[k - 1] + acc.area() * c;
+                if (s < best) best = s, best_axis = ax, best_bin = k;
+            }
+        }
+        float area = bounds(a, b).area();
+        float split_cost = (best_axis >= 0 && area > 0) ? 0.5f * cost_leaf / n + best / area : INFINITY;
+        if (n <= kMaxLeaf && split_cost >= cost_leaf) return -1;
+        if (best_axis < 0) {                         // all centroids coincide
+            if (n <= 15) return -1;
+            return a + n / 2;
+        }
+        float lo = cb.lo[best_axis], scale = kBins / (cb.hi[best_axis] - lo);
+        auto it = std::partition(idx.begin() + a, idx.begin() + b, [&](int i) {
+            int k = std::min(kBins - 1, std::max(0, (int)((P[i].c[best_axis] - lo) * scale)));
+            return k < best_bin;
+        });
+        int mid = (int)(it - idx.begin());
+        if (mid == a || mid == b) mid = a + n / 2;
+        return mid;
+    }
+
+    int32_t build_range(int a, int b, int depth) {
+        out->depth = std::max(out->depth, depth);
+        int mid = split_point(a, b, depth);
+        if (mid < 0) return leaf_link(a, b - a);
+        int ni = (int)out->nodes.size();
+        out->nodes.emplace_back();
+        int32_t l = build_range(a, mid, depth + 1);
+        int32_t r = build_range(mid, b, depth + 1);
+        set_child(out->nodes[ni], 0, bounds(a, mid), l);
+        set_child(out->nodes[ni], 1, bounds(mid, b), r);
+        return ni;
+    }
+};
+
+}  // namespace rtbvh

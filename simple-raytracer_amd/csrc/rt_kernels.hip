@@ -35,6 +35,7 @@
 #include <string>
 #include <vector>
 
+#include "rt_bvh.h"
 #include "rt_hip.h"
 
 namespace rt {
@@ -140,7 +141,16 @@ struct Params {
     float eye[3], ul[3], dh[3], dv[3];
     int W, y0, rows;                     // render rows [y0, y0 + rows) of a W-wide image
     unsigned int total;                  // W * rows
+    // BVH (MODE_BVH): 4 float4 per node (rt_bvh.h Node), leaf-ordered object keys
+    const float4 *__restrict__ bvh;
+    const int *__restrict__ bkeys;
+    int dir_bf;                          // directional shadow rays must scan spheres brute force
+    int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
 };
+
+enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
+constexpr int kStack = 40;               // per-lane BVH stack entries (rtbvh::Builder::kMaxDepth)
+constexpr int kBlock = 256;
 
 // ---------------------------------------------------------------------------
 // One lane's ray query (a TraceRay call + the consumer loop that follows it)
@@ -156,6 +166,7 @@ struct Query {
     float tmin, tmax;
     int self, back, win;
     bool closest, unb, skipchk, skipped;
+    bool bf;                              // BVH mode: this query needs the brute-force scan
     C3 mask;
 };
 
@@ -216,7 +227,11 @@ __device__ __forceinline__ bool sphere_test(float4 s, V3 o, V3 d, float &t1, flo
 // The scan every active lane of the wave runs together.  SRC_LDS: primitive
 // arrays were staged into LDS (lds_f, lds_s); otherwise scalar loads.
 template <bool SRC_LDS>
-__device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s) {
+__device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s,
+                                     bool part, unsigned long long &ft, unsigned long long &st) {
+    if (!part) return;
+    ft += (unsigned long long)p.nf;
+    st += (unsigned long long)p.ns;
     for (int i = 0; i < p.nf; i++) {
         float4 f0, f1, f2, f3, f4;
         if (SRC_LDS) {
@@ -244,6 +259,145 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// BVH traversal (MODE_BVH).  Candidates come from the BVH in any order; the
+// reference's sequential semantics are restored exactly:
+//   closest : keep the smallest t, ties -> smallest object index (= the
+//             reference's first-in-order winner under its strict '<');
+//   shadow  : valid hits are recorded and multiplied into the mask in object
+//             order (both roots of a sphere are adjacent); an opaque hit
+//             zeroes the mask whatever the order (when no factor is NaN).
+// Queries the BVH cannot reproduce (SKIP_TRANS checks, directional shadow
+// rays against spheres, > kHits semi-transparent shadow hits) set q.bf and are
+// re-run by the brute-force scan.
+// ---------------------------------------------------------------------------
+struct Counters {
+    unsigned prim, shadow, refr, refl, skip, ub;
+    unsigned long long boxes, ftests, stests;   // ray-box, ray-face, ray-sphere tests executed
+};
+
+constexpr int kHits = 8;
+
+__device__ __forceinline__ float safe_rcp(float x) {
+    return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
+}
+
+__device__ __forceinline__ void slab(float lx, float ly, float lz, float hx, float hy, float hz, float ix, float iy,
+                                     float iz, float ox, float oy, float oz, float tlo, float thi, float &tn, float &tf) {
+    float t0x = fmaf(lx, ix, -ox), t1x = fmaf(hx, ix, -ox);
+    float t0y = fmaf(ly, iy, -oy), t1y = fmaf(hy, iy, -oy);
+    float t0z = fmaf(lz, iz, -oz), t1z = fmaf(hz, iz, -oz);
+    tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tlo));
+    tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
+}
+
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
+    const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
+    const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
+    const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
+    float best = q.tmax;                       // closest: running min (kFltMax at start)
+    int win = -1;
+    int nh = 0;
+    int hkey[kHits];
+    float hf[kHits];
+    bool opaque = false;
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        if (node >= 0) {
+            const float4 *N = p.bvh + 4 * node;
+            float4 a = N[0], b = N[1], c = N[2];
+            int4 l = *reinterpret_cast<const int4 *>(N + 3);
+            float thi = q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
+            float tnl, tfl, tnr, tfr;
+            slab(a.x, a.y, a.z, a.w, b.x, b.y, ix, iy, iz, ox, oy, oz, tlo, thi, tnl, tfl);
+            slab(b.z, b.w, c.x, c.y, c.z, c.w, ix, iy, iz, ox, oy, oz, tlo, thi, tnr, tfr);
+            cnt.boxes += 2;
+            bool hl = tnl <= tfl, hr = tnr <= tfr;
+            if (hl && hr) {
+                bool lfirst = tnl <= tnr;
+                stk[sp * kBlock] = lfirst ? l.y : l.x;
+                sp++;
+                node = lfirst ? l.x : l.y;
+                continue;
+            }
+            if (hl | hr) {
+                node = hl ? l.x : l.y;
+                continue;
+            }
+        } else {
+            int v = -node - 1;
+            int first = v >> 4, count = v & 15;
+            for (int k = first; k < first + count; k++) {
+                int key = p.bkeys[k];
+                float t[2];
+                int nt = 0;
+                if (key < p.nf) {
+                    const float4 *F = p.fscan + 5 * key;
+                    float a, bb, g;
+                    cnt.ftests++;
+                    if (F[1].w != 0.0f && face_test(F[0], F[1], F[2], F[3], F[4], q.o, q.d, t[0], a, bb, g)) nt = 1;
+                } else {
+                    cnt.stests++;
+                    if (sphere_test(p.sscan[key - p.nf], q.o, q.d, t[0], t[1])) nt = 2;
+                }
+                for (int r = 0; r < nt; r++) {
+                    float tt = t[r];
+                    if (q.closest) {
+                        bool valid = (tt > q.tmin) & (tt < kFltMax);
+                        bool better = (tt < best) | ((tt == best) & (key < win));
+                        if (valid & better) {
+                            best = tt;
+                            win = key;
+                        }
+                    } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
+                        float f = cst(p.ofac)[key];
+                        if (f == 0.0f && p.shadow_early_out) {
+                            opaque = true;
+                        } else if (nh < kHits) {
+                            hkey[nh] = key;
+                            hf[nh] = f;
+                            nh++;
+                        } else {
+                            q.bf = true;           // too many: let the scan redo it in order
+                        }
+                    }
+                }
+            }
+            if (opaque || q.bf) break;
+        }
+        if (sp == 0) break;
+        sp--;
+        node = stk[sp * kBlock];
+    }
+    if (q.closest) {
+        if (win >= 0) {
+            q.tmax = best;
+            q.win = win;
+        }
+    } else if (!q.bf) {
+        if (opaque) {
+            q.mask = {0.0f, 0.0f, 0.0f};
+        } else {
+            // multiply in object order (insertion sort; nh <= kHits)
+            for (int i = 1; i < nh; i++) {
+                int k = hkey[i];
+                float f = hf[i];
+                int j = i - 1;
+                while (j >= 0 && hkey[j] > k) {
+                    hkey[j + 1] = hkey[j];
+                    hf[j + 1] = hf[j];
+                    j--;
+                }
+                hkey[j + 1] = k;
+                hf[j + 1] = f;
+            }
+            for (int i = 0; i < nh; i++) q.mask = cmulf(q.mask, hf[i]);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // ShadeRay as a per-lane state machine
 // ---------------------------------------------------------------------------
@@ -260,9 +414,6 @@ struct Frame {
     float Ft;                        // transmission Fresnel F (main.cpp:966)
 };
 
-struct Counters {
-    unsigned prim, shadow, refr, refl, skip, ub;
-};
 
 // Hit record of the winning intersection, recomputed exactly as TraceRay did.
 __device__ void hit_geometry(const Params &p, int obj, V3 o, V3 d, float t, V3 &P, V3 &N, V3 &bary) {
@@ -652,8 +803,9 @@ __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, 
     y = (int)s * 8 + (int)(r % (unsigned)sh);
 }
 
-template <int MAXF, bool SRC_LDS>
-__global__ void __launch_bounds__(256) render_kernel(Params p) {
+template <int MAXF, int MODE>
+__global__ void __launch_bounds__(kBlock, 3) render_kernel(Params p) {
+    constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
     extern __shared__ float4 lds[];
     const float4 *lds_f = lds;
     const float4 *lds_s = lds + 5 * p.nf;
@@ -666,7 +818,8 @@ __global__ void __launch_bounds__(256) render_kernel(Params p) {
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
-    Counters cnt = {0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;   // MODE_BVH: stack[k * kBlock]
     Query q;
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
@@ -722,7 +875,14 @@ __global__ void __launch_bounds__(256) render_kernel(Params p) {
         }
         if (!pending) q.tmin = kInf;                 // lane sits this scan out
         if (__ballot(pending) == 0ull) break;
-        scan<SRC_LDS>(q, p, lds_f, lds_s);
+        if (MODE == MODE_BVH) {
+            q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+            if (pending && !q.bf) bvh_trace(q, p, stk, cnt);
+            bool need = pending && q.bf;
+            if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
+        } else {
+            scan<SRC_LDS>(q, p, lds_f, lds_s, pending, cnt.ftests, cnt.stests);
+        }
     }
     unsigned long long *st = p.stats;
     atomicAdd(&st[0], (unsigned long long)cnt.prim);
@@ -731,6 +891,9 @@ __global__ void __launch_bounds__(256) render_kernel(Params p) {
     atomicAdd(&st[3], (unsigned long long)cnt.refl);
     atomicAdd(&st[4], (unsigned long long)cnt.skip);
     atomicAdd(&st[5], (unsigned long long)cnt.ub);
+    atomicAdd(&st[6], cnt.boxes);
+    atomicAdd(&st[7], cnt.ftests);
+    atomicAdd(&st[8], cnt.stests);
 }
 
 }  // namespace rt
@@ -754,6 +917,22 @@ struct rt_scene {
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
+    long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
+    // BVH inputs kept on the host (the boxes' padding depends on the eye)
+    struct PrimSrc {
+        int key;
+        bool sphere;
+        float lo[3], hi[3];            // face: vertex bounds; sphere: centre +- r
+        float c[3], r;                 // sphere centre / radius
+        double cond;                   // face: |e1|^2 |e2|^2 / det
+    };
+    std::vector<PrimSrc> prims;
+    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
+    double bvh_D = -1.0;               // distance bound the current BVH was padded for
+    float4 *d_bvh = nullptr;
+    int *d_bkeys = nullptr;
+    int bvh_depth = 0;
+    bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
     bool last_valid = false;
 };
@@ -777,40 +956,133 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
 
 V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
-template <int MAXF, bool LDS>
-hipError_t launch_one(rt_scene *s, const Params &p, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((render_kernel<MAXF, LDS>), dim3(grid), dim3(256), LDS ? s->lds_bytes : 0, st, p);
+size_t mode_lds_bytes(const rt_scene *s, int mode) {
+    if (mode == MODE_SCAN_LDS) return s->lds_bytes;
+    if (mode == MODE_BVH) return (size_t)kStack * kBlock * sizeof(int);
+    return 0;
+}
+
+template <int MAXF, int MODE>
+hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
+    size_t shm = mode_lds_bytes(s, MODE);
+    int nb = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE>, kBlock, shm);
+    if (nb < 1) nb = 1;
+    long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu;
+    long long need = ((long long)p.total + kBlock - 1) / kBlock;
+    if (grid > need) grid = need;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, p);
     return hipGetLastError();
 }
 
 template <int MAXF>
-int occupancy(rt_scene *s, bool lds) {
-    int nb = 0;
-    if (lds)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, true>, 256, s->lds_bytes);
-    else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, false>, 256, 0);
-    return nb;
+hipError_t launch_mode(rt_scene *s, const Params &p, int mode, hipStream_t st) {
+    if (mode == MODE_BVH) return launch_one<MAXF, MODE_BVH>(s, p, st);
+    if (mode == MODE_SCAN_LDS) return launch_one<MAXF, MODE_SCAN_LDS>(s, p, st);
+    return launch_one<MAXF, MODE_SCAN>(s, p, st);
+}
+
+// Distance bound for the BVH padding: from any ray origin (the eye, or a point
+// inside the scene's bounds) to any primitive.
+double distance_bound(const rt_scene *s, const float eye[3]) {
+    double diag2 = 0, far2 = 0, mag = 0;
+    for (int k = 0; k < 3; k++) {
+        double e = s->scene_hi[k] - s->scene_lo[k];
+        diag2 += e * e;
+        double a = std::fabs(eye[k] - s->scene_lo[k]), b = std::fabs(eye[k] - s->scene_hi[k]);
+        far2 += std::max(a, b) * std::max(a, b);
+        mag = std::max(mag, std::max(std::fabs((double)s->scene_lo[k]), std::fabs((double)s->scene_hi[k])));
+        mag = std::max(mag, std::fabs((double)eye[k]));
+    }
+    return std::max(std::sqrt(diag2), std::sqrt(far2)) + mag + 1.0;
+}
+
+// (Re)build the BVH with boxes padded for distance bound D (see rt_bvh.h):
+//   face   pad = 2^-16 * D * max(1, cond)                 (32x the rounding bound)
+//   sphere radius' = sqrt(r^2 + 2^-18 D^2) + 2^-16 D     (discriminant error)
+int build_bvh(rt_scene *s, double D) {
+    std::vector<rtbvh::Prim> P(s->prims.size());
+    for (size_t i = 0; i < P.size(); i++) {
+        const auto &src = s->prims[i];
+        rtbvh::Prim &q = P[i];
+        q.key = src.key;
+        if (!src.sphere) {
+            double pad = std::ldexp(D, -16) * std::max(1.0, src.cond);
+            for (int k = 0; k < 3; k++) {
+                q.box.lo[k] = (float)(src.lo[k] - pad);
+                q.box.hi[k] = (float)(src.hi[k] + pad);
+                q.c[k] = 0.5f * (src.lo[k] + src.hi[k]);
+            }
+            q.cost = 3.0f;
+        } else {
+            double r = std::fabs((double)src.r);
+            double rr = std::sqrt(r * r + std::ldexp(D * D, -18)) + std::ldexp(D, -16);
+            for (int k = 0; k < 3; k++) {
+                q.box.lo[k] = (float)(src.c[k] - rr);
+                q.box.hi[k] = (float)(src.c[k] + rr);
+                q.c[k] = src.c[k];
+            }
+            q.cost = 1.0f;
+        }
+        // float rounding of the padded box must not shrink it
+        for (int k = 0; k < 3; k++) {
+            q.box.lo[k] = std::nextafter(q.box.lo[k], -INFINITY);
+            q.box.hi[k] = std::nextafter(q.box.hi[k], INFINITY);
+            if (!std::isfinite(q.box.lo[k]) || !std::isfinite(q.box.hi[k])) {
+                q.box.lo[k] = -INFINITY;   // NaN/inf geometry: a box every ray enters
+                q.box.hi[k] = INFINITY;
+            }
+        }
+    }
+    rtbvh::Result R;
+    rtbvh::Builder B(P);
+    bool ok = B.build(R);
+    s->bvh_depth = R.depth;
+    s->bvh_ok = ok && !R.nodes.empty();
+    s->bvh_D = D;
+    if (!s->bvh_ok) return RT_OK;                              // fall back to the scan
+    if (s->d_bvh) (void)hipFree(s->d_bvh);
+    if (s->d_bkeys) (void)hipFree(s->d_bkeys);
+    s->d_bvh = nullptr;
+    s->d_bkeys = nullptr;
+    if (hipMalloc(&s->d_bvh, R.nodes.size() * sizeof(rtbvh::Node)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&s->d_bkeys, R.keys.size() * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMemcpy(s->d_bvh, R.nodes.data(), R.nodes.size() * sizeof(rtbvh::Node), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s->d_bkeys, R.keys.data(), R.keys.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+        return RT_E_HIP;
+    s->base.bvh = s->d_bvh;
+    s->base.bkeys = s->d_bkeys;
+    return RT_OK;
 }
 
 int launch(rt_scene *s, Params &p, hipStream_t st) {
-    bool lds = s->opt_lds == 1 || (s->opt_lds == -1 && s->lds_bytes <= 64 * 1024);
-    if (s->lds_bytes > 160 * 1024) lds = false;
     int depth = p.depth < 0 ? 0 : p.depth;
-    int nb;
-    if (depth <= 4) nb = occupancy<5>(s, lds);
-    else if (depth <= 8) nb = occupancy<9>(s, lds);
-    else if (depth <= 16) nb = occupancy<17>(s, lds);
-    else return RT_E_UNSUPPORTED;
-    if (nb < 1) nb = 1;
-    long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu;
-    long long need = ((long long)p.total + 255) / 256;
-    if (grid > need) grid = need;
-    if (grid < 1) grid = 1;
+    if (depth > 16) return RT_E_UNSUPPORTED;
+    int nobj = p.nf + p.ns;
+    bool bvh = s->opt_accel == 1 || (s->opt_accel == -1 && nobj > 32);
+    int mode = MODE_SCAN;
+    if (bvh) {
+        double D = distance_bound(s, p.eye);
+        if (D > s->bvh_D) {
+            int rc = build_bvh(s, std::max(D, 1.5 * s->bvh_D));
+            if (rc) return rc;
+        }
+        if (s->bvh_ok) {
+            mode = MODE_BVH;
+            p.bvh = s->base.bvh;
+            p.bkeys = s->base.bkeys;
+        }
+    }
+    if (mode == MODE_SCAN) {
+        bool lds = s->opt_lds == 1 || (s->opt_lds == -1 && s->lds_bytes <= 64 * 1024);
+        if (s->lds_bytes > 64 * 1024) lds = false;
+        if (lds) mode = MODE_SCAN_LDS;
+    }
     hipError_t e;
-    if (depth <= 4) e = lds ? launch_one<5, true>(s, p, (int)grid, st) : launch_one<5, false>(s, p, (int)grid, st);
-    else if (depth <= 8) e = lds ? launch_one<9, true>(s, p, (int)grid, st) : launch_one<9, false>(s, p, (int)grid, st);
-    else e = lds ? launch_one<17, true>(s, p, (int)grid, st) : launch_one<17, false>(s, p, (int)grid, st);
+    if (depth <= 4) e = launch_mode<5>(s, p, mode, st);
+    else if (depth <= 8) e = launch_mode<9>(s, p, mode, st);
+    else e = launch_mode<17>(s, p, mode, st);
     return e == hipSuccess ? RT_OK : RT_E_HIP;
 }
 
@@ -890,12 +1162,48 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
         fs.smooth = F.smooth;
         fill_obj(i, F.mat, F.texture, 0);
     }
+    // BVH sources (padding is applied per build, it depends on the eye)
+    s->prims.reserve((size_t)nobj);
+    for (int i = 0; i < nf; i++) {
+        rt_scene::PrimSrc ps{};
+        ps.key = i;
+        ps.sphere = false;
+        const rt_face_desc &F = desc->faces[i];
+        for (int k = 0; k < 3; k++) {
+            ps.lo[k] = std::min(F.v[0][k], std::min(F.v[1][k], F.v[2][k]));
+            ps.hi[k] = std::max(F.v[0][k], std::max(F.v[1][k], F.v[2][k]));
+        }
+        float4 a = fscan[5 * i + 1], b2 = fscan[5 * i + 2], c2 = fscan[5 * i + 3];
+        double det = a.w, d11 = b2.w, d22 = c2.w;
+        ps.cond = det > 0 ? d11 * d22 / det : 1e30;
+        s->prims.push_back(ps);
+    }
     std::vector<float4> sscan((size_t)ns);
     for (int i = 0; i < ns; i++) {
         const rt_sphere_desc &S = desc->spheres[i];
         sscan[i] = make_float4(S.center[0], S.center[1], S.center[2], S.radius);
         fill_obj(nf + i, S.mat, S.texture, 1);
+        rt_scene::PrimSrc ps{};
+        ps.key = nf + i;
+        ps.sphere = true;
+        for (int k = 0; k < 3; k++) {
+            ps.c[k] = S.center[k];
+            ps.lo[k] = S.center[k] - std::fabs(S.radius);
+            ps.hi[k] = S.center[k] + std::fabs(S.radius);
+        }
+        ps.r = S.radius;
+        s->prims.push_back(ps);
     }
+    for (int k = 0; k < 3; k++) s->scene_lo[k] = INFINITY, s->scene_hi[k] = -INFINITY;
+    for (const auto &ps : s->prims)
+        for (int k = 0; k < 3; k++) {
+            if (std::isfinite(ps.lo[k])) s->scene_lo[k] = std::min(s->scene_lo[k], ps.lo[k]);
+            if (std::isfinite(ps.hi[k])) s->scene_hi[k] = std::max(s->scene_hi[k], ps.hi[k]);
+        }
+    for (int k = 0; k < 3; k++)
+        if (!(s->scene_lo[k] <= s->scene_hi[k])) s->scene_lo[k] = s->scene_hi[k] = 0.0f;
+    bool nan_fac = false;
+    for (float f : ofac) nan_fac |= std::isnan(f);
     std::vector<LightK> lights((size_t)desc->n_lights);
     for (int i = 0; i < desc->n_lights; i++) {
         const rt_light_desc &L = desc->lights[i];
@@ -928,7 +1236,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
     if (!rc && hipMalloc(&s->work, sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
-    if (!rc && hipMalloc(&s->stats, 8 * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
+    if (!rc && hipMalloc(&s->stats, 16 * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
     if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
     if (!rc && (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)) rc = RT_E_HIP;
     if (!rc) {
@@ -949,6 +1257,10 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.depth = desc->depth;
     p.work = s->work;
     p.stats = s->stats;
+    p.dir_bf = 0;
+    for (int i = 0; i < desc->n_lights; i++)
+        if (desc->lights[i].w == 0.0f && ns > 0) p.dir_bf = 1;
+    p.shadow_early_out = nan_fac ? 0 : 1;
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
     *out = s;
     return RT_OK;
@@ -959,6 +1271,8 @@ int rt_scene_destroy(rt_scene *s) {
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void *d : s->allocs) (void)hipFree(d);
+    if (s->d_bvh) (void)hipFree(s->d_bvh);
+    if (s->d_bkeys) (void)hipFree(s->d_bkeys);
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);
@@ -975,6 +1289,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     if (k == "lds") s->opt_lds = value;
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
+    else if (k == "accel") s->opt_accel = value;
     else return RT_E_INVALID;
     return RT_OK;
 }
@@ -998,7 +1313,7 @@ int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0
     p.total = (unsigned)((long long)W * (y1 - y0));
     p.out = out_rgb;
     if (hipMemsetAsync(s->work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
-    if (hipMemsetAsync(s->stats, 0, 8 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    if (hipMemsetAsync(s->stats, 0, 16 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
     (void)hipEventRecord(s->ev0, st);
     int rc = launch(s, p, st);
     (void)hipEventRecord(s->ev1, st);
@@ -1012,7 +1327,7 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     if (!s->last_valid) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
-    unsigned long long h[8];
+    unsigned long long h[16];
     if (hipMemcpy(h, s->stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
     stats->primary = h[0];
     stats->shadow = h[1];
@@ -1020,6 +1335,9 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     stats->reflection = h[3];
     stats->skip_trans = h[4];
     stats->ub_back = h[5];
+    stats->box_tests = h[6];
+    stats->face_tests = h[7];
+    stats->sphere_tests = h[8];
     float ms = 0;
     (void)hipEventElapsedTime(&ms, s->ev0, s->ev1);
     stats->kernel_ms = ms;

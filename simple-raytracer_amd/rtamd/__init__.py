@@ -69,7 +69,8 @@ class rt_stats(C.Structure):
     _fields_ = [("primary", C.c_ulonglong), ("shadow", C.c_ulonglong),
                 ("refraction", C.c_ulonglong), ("reflection", C.c_ulonglong),
                 ("skip_trans", C.c_ulonglong), ("ub_back", C.c_ulonglong),
-                ("kernel_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("box_tests", C.c_ulonglong),
+                ("face_tests", C.c_ulonglong), ("sphere_tests", C.c_ulonglong)]
 
     def rays(self) -> int:
         return int(self.primary + self.shadow + self.refraction + self.reflection)
@@ -284,8 +285,10 @@ class GpuScene:
 
 
 def render_scene(path: str, cwd: str | None = None, device: int = 0, depth: int | None = None,
-                 imsize: tuple[int, int] | None = None, rows: tuple[int, int] | None = None):
-    """Parse + render a scene file on the GPU: returns (float32 HxWx3, rt_stats)."""
+                 imsize: tuple[int, int] | None = None, rows: tuple[int, int] | None = None,
+                 options: dict | None = None):
+    """Parse + render a scene file on the GPU: returns (float32 HxWx3, rt_stats).
+    `options` are rt_scene_set_option knobs, e.g. {"accel": 1}."""
     hs = HostScene(path, cwd=cwd)
     if depth is not None:
         hs.set_depth(depth)
@@ -295,6 +298,8 @@ def render_scene(path: str, cwd: str | None = None, device: int = 0, depth: int 
     cam = hs.camera(W, H)
     y0, y1 = rows if rows else (0, H)
     gs = GpuScene(hs, device)
+    for k, v in (options or {}).items():
+        gs.set_option(k, v)
     try:
         img, st = gs.render_rows(cam, W, H, y0, y1)
     finally:

@@ -1,0 +1,82 @@
+// Structural check of the BVH builder (rt_bvh.h), run by tests/test_bvh_host.py.
+// Reads "n seed mode" from argv, builds over random boxes, verifies:
+//   keys are a permutation; links in range; leaf counts <= 15; every stored
+//   child box contains everything below it; depth <= kMaxDepth.
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../simple-raytracer_amd/csrc/rt_bvh.h"
+
+using namespace rtbvh;
+
+static bool contains(const float lo[3], const float hi[3], const Box &b) {
+    for (int k = 0; k < 3; k++)
+        if (b.lo[k] < lo[k] || b.hi[k] > hi[k]) return false;
+    return true;
+}
+
+int main(int argc, char **argv) {
+    int n = argc > 1 ? atoi(argv[1]) : 1000;
+    int seed = argc > 2 ? atoi(argv[2]) : 1;
+    int mode = argc > 3 ? atoi(argv[3]) : 0;   // 0 random, 1 all coincident, 2 a line
+    std::mt19937 rng(seed);
+    std::uniform_real_distribution<float> U(-20, 20), S(0.1f, 2.0f);
+    std::vector<Prim> P(n);
+    for (int i = 0; i < n; i++) {
+        float c[3] = {U(rng), U(rng), U(rng)};
+        if (mode == 1) c[0] = c[1] = c[2] = 1.0f;
+        if (mode == 2) c[0] = (float)i, c[1] = c[2] = 0.0f;
+        float r = S(rng);
+        for (int k = 0; k < 3; k++) P[i].box.lo[k] = c[k] - r, P[i].box.hi[k] = c[k] + r, P[i].c[k] = c[k];
+        P[i].cost = (i & 1) ? 3.0f : 1.0f;
+        P[i].key = i;
+    }
+    std::vector<Prim> orig = P;
+    Result R;
+    Builder B(P);
+    bool ok = B.build(R);
+    if (!ok) { printf("FAIL depth %d\n", R.depth); return 1; }
+    std::vector<int> seen(n, 0);
+    for (int k : R.keys) {
+        if (k < 0 || k >= n) { printf("FAIL key range\n"); return 1; }
+        seen[k]++;
+    }
+    for (int i = 0; i < n; i++)
+        if (seen[i] != 1) { printf("FAIL key %d seen %d\n", i, seen[i]); return 1; }
+    // walk
+    struct It { int link; float lo[3], hi[3]; int depth; };
+    std::vector<It> st;
+    const Node &r = R.nodes[0];
+    float inf = INFINITY;
+    It root{0, {-inf, -inf, -inf}, {inf, inf, inf}, 1};
+    st.push_back(root);
+    int leaves = 0, covered = 0, maxd = 0;
+    while (!st.empty()) {
+        It it = st.back();
+        st.pop_back();
+        maxd = std::max(maxd, it.depth);
+        if (it.link >= 0) {
+            if (it.link >= (int)R.nodes.size()) { printf("FAIL node range\n"); return 1; }
+            const Node &nd = R.nodes[it.link];
+            float l_lo[3] = {nd.l_lo[0], nd.l_lo[1], nd.l_lo[2]}, l_hi[3] = {nd.l_hi0, nd.l_hi12[0], nd.l_hi12[1]};
+            float r_lo[3] = {nd.r_lo01[0], nd.r_lo01[1], nd.r_lo2}, r_hi[3] = {nd.r_hi[0], nd.r_hi[1], nd.r_hi[2]};
+            It a{nd.link[0], {}, {}, it.depth + 1}, b{nd.link[1], {}, {}, it.depth + 1};
+            for (int k = 0; k < 3; k++) a.lo[k] = l_lo[k], a.hi[k] = l_hi[k], b.lo[k] = r_lo[k], b.hi[k] = r_hi[k];
+            st.push_back(a);
+            st.push_back(b);
+        } else {
+            int v = -it.link - 1, first = v >> 4, count = v & 15;
+            if (first < 0 || first + count > n) { printf("FAIL leaf range\n"); return 1; }
+            leaves++;
+            covered += count;
+            for (int q = first; q < first + count; q++)
+                if (!contains(it.lo, it.hi, orig[R.keys[q]].box)) { printf("FAIL containment\n"); return 1; }
+        }
+    }
+    if (covered != n) { printf("FAIL covered %d of %d\n", covered, n); return 1; }
+    (void)r;
+    printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d\n", n, R.nodes.size(), leaves, R.depth, maxd);
+    return 0;
+}
