@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "simple-raytracer_amd"))
 PEAK_FP32_TFLOPS = 157.3        # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBPS = 8000.0          # HBM3E spec
 FLOP_SPHERE, FLOP_TRI = 20, 42  # algorithmic FLOPs per ray-primitive test
+FLOP_BOX = 22                   # ray-AABB slab test: 6 FMA (12) + 10 min/max
 
 WORKLOADS = {
     "C2": "C2: 1024x1024, 100 spheres, 2 point lights, no reflection/refraction",
@@ -185,11 +186,14 @@ def main() -> None:
     if rank == 0:
         value = rays_total * args.steps / elapsed / 1e6
         ns, nt = cfg["spheres"], cfg["tris"]
-        flop_per_ray = FLOP_SPHERE * ns + FLOP_TRI * nt
-        # dominant kernel = render_kernel; per launch on rank 0 (its strip)
+        bf_flop_per_ray = FLOP_SPHERE * ns + FLOP_TRI * nt
+        # dominant kernel = render_kernel; per launch on rank 0 (its strip).
+        # achieved = FLOPs of the tests the launch executed (ray-box + ray-face +
+        # ray-sphere, counted by the kernel) / its average launch time.
         k_s = float(np.mean(kernel_ms)) / 1e3
-        flops = my_rays * flop_per_ray
+        flops = st.box_tests * FLOP_BOX + st.face_tests * FLOP_TRI + st.sphere_tests * FLOP_SPHERE
         achieved = flops / k_s / 1e12
+        bf_equiv = my_rays * bf_flop_per_ray / k_s / 1e12
         px = (y1 - y0) * W
         scene_bytes = 80 * nt + 16 * ns + 52 * (ns + nt)
         alg_bytes = 12 * px + scene_bytes
@@ -224,7 +228,13 @@ def main() -> None:
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic, "kernel": "render_kernel",
                          "kernel_ms": round(float(np.mean(kernel_ms)), 3),
-                         "flop_per_ray": flop_per_ray, "rays_per_launch": my_rays,
+                         "rays_per_launch": my_rays,
+                         "tests_per_launch": {"box": st.box_tests, "face": st.face_tests,
+                                              "sphere": st.sphere_tests},
+                         "flop_per_test": {"box": FLOP_BOX, "face": FLOP_TRI, "sphere": FLOP_SPHERE},
+                         "brute_force_equivalent": {"flop_per_ray": bf_flop_per_ray,
+                                                    "TFLOPs": round(bf_equiv, 3),
+                                                    "frac": round(bf_equiv / PEAK_FP32_TFLOPS, 4)},
                          "hbm": {"alg_bytes_per_launch": alg_bytes,
                                  "achieved_GBps": round(alg_bytes / k_s / 1e9, 3),
                                  "peak_GBps": PEAK_HBM_GBPS,

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 namespace rtbvh {
@@ -67,10 +68,88 @@ struct Result {
 
 inline int32_t leaf_link(int first, int count) { return -(1 + ((first << 4) | count)); }
 
+// 4-wide node (128 B): the children's boxes as SoA rows + links.  Unused
+// slots carry link kEmpty.  Built by collapsing the binary tree (each node
+// absorbs grandchildren, largest surface area first).
+constexpr int32_t kEmpty = INT32_MIN;
+struct Node4 {
+    float lo[3][4];
+    float hi[3][4];
+    int32_t link[4];
+    int32_t max_stack;       // worst-case traversal stack entries below (root only)
+    int32_t pad[3];
+};
+static_assert(sizeof(Node4) == 128, "node4 layout");
+
+struct Result4 {
+    std::vector<Node4> nodes;
+    int depth = 0;
+    int max_stack = 0;       // worst-case entries a near-first traversal pushes
+};
+
+// Collapse a binary tree (Result) into 4-wide nodes.
+inline void collapse4(const Result &R, Result4 &Q) {
+    Q = Result4();
+    if (R.nodes.empty()) return;
+    struct Child {
+        int32_t link;
+        Box box;
+    };
+    auto children2 = [&](int ni, Child out[2]) {
+        const Node &n = R.nodes[ni];
+        out[0].link = n.link[0];
+        out[1].link = n.link[1];
+        for (int k = 0; k < 3; k++) out[0].box.lo[k] = n.l_lo[k];
+        out[0].box.hi[0] = n.l_hi0, out[0].box.hi[1] = n.l_hi12[0], out[0].box.hi[2] = n.l_hi12[1];
+        out[1].box.lo[0] = n.r_lo01[0], out[1].box.lo[1] = n.r_lo01[1], out[1].box.lo[2] = n.r_lo2;
+        for (int k = 0; k < 3; k++) out[1].box.hi[k] = n.r_hi[k];
+    };
+    // returns the node4 index; `stack_in` = entries already on the stack on entry
+    std::function<int(int, int, int)> conv = [&](int ni, int depth, int stack_in) -> int {
+        Child ch[4];
+        int n = 2;
+        children2(ni, ch);
+        for (;;) {
+            if (n == 4) break;
+            int best = -1;
+            float ba = -1;
+            for (int i = 0; i < n; i++)
+                if (ch[i].link >= 0 && ch[i].box.area() > ba) ba = ch[i].box.area(), best = i;
+            if (best < 0) break;
+            Child g[2];
+            children2(ch[best].link, g);
+            ch[best] = g[0];
+            ch[n++] = g[1];
+        }
+        int qi = (int)Q.nodes.size();
+        Q.nodes.emplace_back();
+        Q.depth = std::max(Q.depth, depth);
+        // near-first traversal: visiting a child keeps up to (hits - 1) siblings on the stack
+        int below = stack_in + (n - 1);
+        Q.max_stack = std::max(Q.max_stack, below);
+        int32_t links[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+        for (int i = 0; i < n; i++) links[i] = ch[i].link >= 0 ? conv(ch[i].link, depth + 1, below) : ch[i].link;
+        Node4 &q = Q.nodes[qi];
+        for (int i = 0; i < 4; i++) {
+            for (int k = 0; k < 3; k++) {
+                q.lo[k][i] = i < n ? ch[i].box.lo[k] : INFINITY;
+                q.hi[k][i] = i < n ? ch[i].box.hi[k] : -INFINITY;
+            }
+            q.link[i] = links[i];
+        }
+        q.max_stack = 0;
+        q.pad[0] = q.pad[1] = q.pad[2] = 0;
+        return qi;
+    };
+    conv(0, 1, 0);
+    Q.nodes[0].max_stack = Q.max_stack;
+}
+
 class Builder {
    public:
     static constexpr int kBins = 32;
-    static constexpr int kMaxLeaf = 8;      // SAH leaves (<= 15 fits the link encoding)
+    int max_leaf = 8;                       // SAH leaves (<= 15 fits the link encoding)
+    float trav_cost = 1.0f;                 // SAH cost of one node visit, in sphere tests
     static constexpr int kSahDepth = 22;    // deeper: object-median splits (bounded depth)
     static constexpr int kMaxDepth = 40;    // the device traversal stack holds 40 entries
 
@@ -174,8 +253,8 @@ class Builder {
             }
         }
         float area = bounds(a, b).area();
-        float split_cost = (best_axis >= 0 && area > 0) ? 0.5f * cost_leaf / n + best / area : INFINITY;
-        if (n <= kMaxLeaf && split_cost >= cost_leaf) return -1;
+        float split_cost = (best_axis >= 0 && area > 0) ? trav_cost + best / area : INFINITY;
+        if (n <= max_leaf && split_cost >= cost_leaf) return -1;
         if (best_axis < 0) {                         // all centroids coincide
             if (n <= 15) return -1;
             return a + n / 2;

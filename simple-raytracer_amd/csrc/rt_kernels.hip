@@ -141,7 +141,7 @@ struct Params {
     float eye[3], ul[3], dh[3], dv[3];
     int W, y0, rows;                     // render rows [y0, y0 + rows) of a W-wide image
     unsigned int total;                  // W * rows
-    // BVH (MODE_BVH): 4 float4 per node (rt_bvh.h Node), leaf-ordered object keys
+    // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
     const int *__restrict__ bkeys;
     int dir_bf;                          // directional shadow rays must scan spheres brute force
@@ -149,7 +149,10 @@ struct Params {
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
-constexpr int kStack = 40;               // per-lane BVH stack entries (rtbvh::Builder::kMaxDepth)
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 3                   // waves per SIMD the register budget must allow
+#endif
+constexpr int kStack = 40;               // max per-lane BVH stack entries; LDS holds the tree's bound
 constexpr int kBlock = 256;
 
 // ---------------------------------------------------------------------------
@@ -306,24 +309,45 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
     int node = 0;
     for (;;) {
         if (node >= 0) {
-            const float4 *N = p.bvh + 4 * node;
-            float4 a = N[0], b = N[1], c = N[2];
-            int4 l = *reinterpret_cast<const int4 *>(N + 3);
+            // 4-wide node: lo.x/y/z rows, hi.x/y/z rows, links (rt_bvh.h Node4)
+            const float4 *N = p.bvh + 8 * node;
+            float4 lx = N[0], ly = N[1], lz = N[2], hx = N[3], hy = N[4], hz = N[5];
+            int4 lk = *reinterpret_cast<const int4 *>(N + 6);
             float thi = q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
-            float tnl, tfl, tnr, tfr;
-            slab(a.x, a.y, a.z, a.w, b.x, b.y, ix, iy, iz, ox, oy, oz, tlo, thi, tnl, tfl);
-            slab(b.z, b.w, c.x, c.y, c.z, c.w, ix, iy, iz, ox, oy, oz, tlo, thi, tnr, tfr);
-            cnt.boxes += 2;
-            bool hl = tnl <= tfl, hr = tnr <= tfr;
-            if (hl && hr) {
-                bool lfirst = tnl <= tnr;
-                stk[sp * kBlock] = lfirst ? l.y : l.x;
-                sp++;
-                node = lfirst ? l.x : l.y;
-                continue;
-            }
-            if (hl | hr) {
-                node = hl ? l.x : l.y;
+            float n0, f0, n1, f1, n2, f2, n3, f3;
+            slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, ix, iy, iz, ox, oy, oz, tlo, thi, n0, f0);
+            slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, ix, iy, iz, ox, oy, oz, tlo, thi, n1, f1);
+            slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, ix, iy, iz, ox, oy, oz, tlo, thi, n2, f2);
+            slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, ix, iy, iz, ox, oy, oz, tlo, thi, n3, f3);
+            cnt.boxes += 4;
+            // entry distance of each hit child, +inf for a miss or an empty slot
+            float k0 = ((n0 <= f0) & (lk.x != rtbvh::kEmpty)) ? n0 : kInf;
+            float k1 = ((n1 <= f1) & (lk.y != rtbvh::kEmpty)) ? n1 : kInf;
+            float k2 = ((n2 <= f2) & (lk.z != rtbvh::kEmpty)) ? n2 : kInf;
+            float k3 = ((n3 <= f3) & (lk.w != rtbvh::kEmpty)) ? n3 : kInf;
+            int c0 = lk.x, c1 = lk.y, c2 = lk.z, c3 = lk.w;
+            // near-first order: 5-comparator sorting network, registers only
+#define RT_CSWAP(ka, ca, kb, cb)                 \
+    {                                            \
+        bool sw = kb < ka;                       \
+        float tk = sw ? kb : ka;                 \
+        kb = sw ? ka : kb;                       \
+        ka = tk;                                 \
+        int tc = sw ? cb : ca;                   \
+        cb = sw ? ca : cb;                       \
+        ca = tc;                                 \
+    }
+            RT_CSWAP(k0, c0, k1, c1);
+            RT_CSWAP(k2, c2, k3, c3);
+            RT_CSWAP(k0, c0, k2, c2);
+            RT_CSWAP(k1, c1, k3, c3);
+            RT_CSWAP(k1, c1, k2, c2);
+#undef RT_CSWAP
+            if (k0 < kInf) {
+                if (k3 < kInf) stk[(sp++) * kBlock] = c3;
+                if (k2 < kInf) stk[(sp++) * kBlock] = c2;
+                if (k1 < kInf) stk[(sp++) * kBlock] = c1;
+                node = c0;
                 continue;
             }
         } else {
@@ -804,7 +828,7 @@ __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, 
 }
 
 template <int MAXF, int MODE>
-__global__ void __launch_bounds__(kBlock, 3) render_kernel(Params p) {
+__global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) {
     constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
     extern __shared__ float4 lds[];
     const float4 *lds_f = lds;
@@ -918,6 +942,8 @@ struct rt_scene {
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
+    long long opt_bvh_leaf = 8;        // SAH max leaf size
+    long long opt_bvh_trav = 1000;     // SAH traversal cost, x1000 of a sphere test
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
     struct PrimSrc {
         int key;
@@ -932,6 +958,7 @@ struct rt_scene {
     float4 *d_bvh = nullptr;
     int *d_bkeys = nullptr;
     int bvh_depth = 0;
+    int bvh_stack = 0;
     bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
     bool last_valid = false;
@@ -958,7 +985,7 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
-    if (mode == MODE_BVH) return (size_t)kStack * kBlock * sizeof(int);
+    if (mode == MODE_BVH) return (size_t)std::max(1, s->bvh_stack) * kBlock * sizeof(int);
     return 0;
 }
 
@@ -1037,18 +1064,24 @@ int build_bvh(rt_scene *s, double D) {
     }
     rtbvh::Result R;
     rtbvh::Builder B(P);
+    B.max_leaf = (int)s->opt_bvh_leaf;
+    B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
     bool ok = B.build(R);
-    s->bvh_depth = R.depth;
-    s->bvh_ok = ok && !R.nodes.empty();
+    rtbvh::Result4 Q;
+    if (ok && !R.nodes.empty()) rtbvh::collapse4(R, Q);
+    s->bvh_depth = Q.depth;
+    s->bvh_stack = Q.max_stack;
+    // the device stack holds kStack entries: a deeper tree uses the scan
+    s->bvh_ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
     s->bvh_D = D;
     if (!s->bvh_ok) return RT_OK;                              // fall back to the scan
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_bkeys) (void)hipFree(s->d_bkeys);
     s->d_bvh = nullptr;
     s->d_bkeys = nullptr;
-    if (hipMalloc(&s->d_bvh, R.nodes.size() * sizeof(rtbvh::Node)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&s->d_bvh, Q.nodes.size() * sizeof(rtbvh::Node4)) != hipSuccess) return RT_E_NOMEM;
     if (hipMalloc(&s->d_bkeys, R.keys.size() * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMemcpy(s->d_bvh, R.nodes.data(), R.nodes.size() * sizeof(rtbvh::Node), hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(s->d_bvh, Q.nodes.data(), Q.nodes.size() * sizeof(rtbvh::Node4), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(s->d_bkeys, R.keys.data(), R.keys.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
         return RT_E_HIP;
     s->base.bvh = s->d_bvh;
@@ -1290,6 +1323,11 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
+    else if (k == "bvh_leaf" || k == "bvh_trav") {
+        if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
+        else s->opt_bvh_trav = std::max(0LL, value);
+        s->bvh_D = -1.0;               // rebuild on the next render
+    }
     else return RT_E_INVALID;
     return RT_OK;
 }

@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_DIR = os.environ.get("RTAMD_LIB_DIR") or os.path.join(PKG_DIR, "lib")   # A/B variants: lib_<x>/
 
 RT_OK = 0
 ERRORS = {-1: "invalid argument", -2: "no such HIP device", -3: "HIP runtime error",

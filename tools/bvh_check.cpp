@@ -77,6 +77,42 @@ int main(int argc, char **argv) {
     }
     if (covered != n) { printf("FAIL covered %d of %d\n", covered, n); return 1; }
     (void)r;
-    printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d\n", n, R.nodes.size(), leaves, R.depth, maxd);
+    // 4-wide collapse: same leaves, contained boxes, every slot valid or empty
+    Result4 Q;
+    collapse4(R, Q);
+    struct It4 { int link; float lo[3], hi[3]; int stack; };
+    std::vector<It4> s4;
+    s4.push_back({0, {-inf, -inf, -inf}, {inf, inf, inf}, 0});
+    int cov4 = 0, maxstack = 0;
+    while (!s4.empty()) {
+        It4 it = s4.back();
+        s4.pop_back();
+        if (it.link >= 0) {
+            if (it.link >= (int)Q.nodes.size()) { printf("FAIL node4 range\n"); return 1; }
+            const Node4 &nd = Q.nodes[it.link];
+            int nch = 0;
+            for (int i = 0; i < 4; i++) nch += nd.link[i] != kEmpty;
+            if (nch < 1) { printf("FAIL empty node4\n"); return 1; }
+            for (int i = 0; i < 4; i++) {
+                if (nd.link[i] == kEmpty) continue;
+                It4 c{nd.link[i], {}, {}, it.stack + nch - 1};
+                maxstack = std::max(maxstack, c.stack);
+                for (int k = 0; k < 3; k++) c.lo[k] = nd.lo[k][i], c.hi[k] = nd.hi[k][i];
+                Box cb;
+                for (int k = 0; k < 3; k++) cb.lo[k] = c.lo[k], cb.hi[k] = c.hi[k];
+                if (!contains(it.lo, it.hi, cb) && it.link != 0) { printf("FAIL node4 containment\n"); return 1; }
+                s4.push_back(c);
+            }
+        } else {
+            int v = -it.link - 1, first = v >> 4, count = v & 15;
+            cov4 += count;
+            for (int q = first; q < first + count; q++)
+                if (!contains(it.lo, it.hi, orig[R.keys[q]].box)) { printf("FAIL leaf4 containment\n"); return 1; }
+        }
+    }
+    if (cov4 != n) { printf("FAIL covered4 %d of %d\n", cov4, n); return 1; }
+    if (maxstack > Q.max_stack || Q.nodes[0].max_stack != Q.max_stack) { printf("FAIL max_stack\n"); return 1; }
+    printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d nodes4=%zu depth4=%d stack4=%d\n", n,
+           R.nodes.size(), leaves, R.depth, maxd, Q.nodes.size(), Q.depth, Q.max_stack);
     return 0;
 }
