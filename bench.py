@@ -156,8 +156,6 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    st = gs.last_stats()
-    my_rays = st.rays()
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
@@ -172,6 +170,8 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in events]
+    st = gs.last_stats()          # counters of the last timed render (identical every step)
+    my_rays = st.rays()
 
     t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms))], dtype=torch.float64, device="cuda")
     if world > 1:

@@ -146,6 +146,13 @@ struct Params {
     const int *__restrict__ bkeys;
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
+    // wavefront engine (engine = 1)
+    struct RayRec *rays;                 // [pixels] the pixel's in-flight ray + frame index
+    void *frames;                        // [pixels][MAXF] Frame<MAXF> (ShadeRay frames in HBM)
+    const int *qin;                      // ray queue (pixel indices), NULL = identity
+    int *qout;
+    const unsigned *cin;                 // queue lengths
+    unsigned *cout;
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -646,16 +653,17 @@ struct LaneState {
 // until the next TraceRay (returns true with q set up) or until the pixel is
 // done (returns false with `color` set).
 template <int MAXF>
-__device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
+__device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &top_ref, Query &q, Counters &cnt,
+                                        C3 &color) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
-    int top = ls.top;
+    int top = top_ref;
     // ---- consume the scan result ----
     if (top < 0) {                                   // primary (main.cpp:729-758)
         if (q.win < 0) {
             color = bkg;
             return false;
         }
-        Frame<MAXF> &f = ls.fr[0];
+        Frame<MAXF> &f = fr[0];
         f.obj = q.win;
         f.ei = p.eta_bkg;
         f.et = p.objs[q.win].eta;
@@ -666,7 +674,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
         node_begin(p, f, q.o, q.d, q.tmax);
         top = 0;
     } else {
-        Frame<MAXF> &f = ls.fr[top];
+        Frame<MAXF> &f = fr[top];
         if (f.phase == PH_LIGHT) {                   // main.cpp:952-958
             f.mask = q.mask;
             const LightK &lt = p.lights[f.light];
@@ -687,7 +695,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
                 cnt.skip++;                          // tmp_transparency stays 0
                 f.phase = PH_REFL;
             } else if (q.win >= 0) {
-                Frame<MAXF> &c = ls.fr[top + 1];
+                Frame<MAXF> &c = fr[top + 1];
                 refr_transition(p, f, c, q.win, cnt);
                 c.obj = q.win;
                 c.depth = f.depth - 1;
@@ -701,7 +709,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
             }
         } else if (f.phase == PH_REFL) {
             if (q.win >= 0) {
-                Frame<MAXF> &c = ls.fr[top + 1];
+                Frame<MAXF> &c = fr[top + 1];
                 refl_transition(p, f, c, q.win);
                 c.obj = q.win;
                 c.depth = f.depth - 1;
@@ -720,7 +728,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
     }
     // ---- run the current frame forward ----
     for (;;) {
-        Frame<MAXF> &f = ls.fr[top];
+        Frame<MAXF> &f = fr[top];
         const ObjK &ob = p.objs[f.obj];
         if (f.phase == PH_LIGHT) {
             if (f.light < p.nl) {                    // shadow ray for light f.light
@@ -740,7 +748,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
                 q.win = -1;
                 q.mask = f.mask;
                 cnt.shadow++;
-                ls.top = top;
+                top_ref = top;
                 return true;
             }
             // ambient + specular sum, then Fresnel / transmission (main.cpp:961-992)
@@ -767,7 +775,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
                 q.win = -1;
                 cnt.refr++;
                 f.phase = PH_REFR;
-                ls.top = top;
+                top_ref = top;
                 return true;
             }
             f.phase = PH_REFL;
@@ -788,7 +796,7 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
                 q.skipped = false;
                 q.win = -1;
                 cnt.refl++;
-                ls.top = top;
+                top_ref = top;
                 return true;
             }
             f.phase = PH_REFL_CHILD + 1;
@@ -797,11 +805,11 @@ __device__ bool advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters
         C3 c = f.acc;
         if (top == 0) {
             color = c;
-            ls.top = -1;
+            top_ref = -1;
             return false;
         }
         top--;
-        Frame<MAXF> &pf = ls.fr[top];
+        Frame<MAXF> &pf = fr[top];
         const ObjK &pob = p.objs[pf.obj];
         if (pf.phase == PH_REFR_CHILD) {             // main.cpp:1072-1083
             C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)pf.Ft)), (float)(1.0 - (double)pob.opacity));
@@ -852,7 +860,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     for (;;) {
         if (pending) {
             C3 color;
-            pending = advance<MAXF>(p, ls, q, cnt, color);
+            pending = advance<MAXF>(p, ls.fr, ls.top, q, cnt, color);
             if (!pending) {
                 float *o = p.out + ((size_t)py * p.W + px) * 3;
                 o[0] = color.r;
@@ -920,6 +928,191 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&st[8], cnt.stests);
 }
 
+
+// ===========================================================================
+// Wavefront engine: the same ShadeRay state machine, one ray per pixel in
+// flight, split into a lean trace kernel and a shade kernel per iteration.
+//   wf_spawn : primary ray of every pixel (main.cpp:720-729)         -> queue
+//   wf_trace : TraceRay for every queued ray (BVH or scan)
+//   wf_shade : consume the result, run ShadeRay to the pixel's next TraceRay
+//              and append it to the next queue (wave ballot + one atomicAdd
+//              + mbcnt prefix), or write the finished pixel
+// Per-pixel state lives in HBM: RayRec (64 B) + MAXF Frame records.
+// ===========================================================================
+struct RayRec {
+    float o[3], d[3];
+    float tmin, tmax;
+    int self, back, win;
+    unsigned flags;          // 1 closest, 2 unb, 4 skipchk, 8 skipped
+    float mask[3];
+    int top;                 // ShadeRay frame index, -1: primary pending
+};
+static_assert(sizeof(RayRec) == 64, "RayRec layout");
+
+__device__ __forceinline__ void ray_load(const RayRec &r, Query &q, int &top) {
+    float4 a = reinterpret_cast<const float4 *>(&r)[0];
+    float4 b = reinterpret_cast<const float4 *>(&r)[1];
+    float4 c = reinterpret_cast<const float4 *>(&r)[2];
+    float4 e = reinterpret_cast<const float4 *>(&r)[3];
+    q.o = {a.x, a.y, a.z};
+    q.d = {a.w, b.x, b.y};
+    q.tmin = b.z;
+    q.tmax = b.w;
+    q.self = __float_as_int(c.x);
+    q.back = __float_as_int(c.y);
+    q.win = __float_as_int(c.z);
+    unsigned fl = __float_as_uint(c.w);
+    q.closest = fl & 1u;
+    q.unb = fl & 2u;
+    q.skipchk = fl & 4u;
+    q.skipped = fl & 8u;
+    q.bf = false;
+    q.mask = {e.x, e.y, e.z};
+    top = __float_as_int(e.w);
+}
+
+__device__ __forceinline__ void ray_store(RayRec &r, const Query &q, int top) {
+    unsigned fl = (q.closest ? 1u : 0u) | (q.unb ? 2u : 0u) | (q.skipchk ? 4u : 0u) | (q.skipped ? 8u : 0u);
+    float4 *w = reinterpret_cast<float4 *>(&r);
+    w[0] = make_float4(q.o.x, q.o.y, q.o.z, q.d.x);
+    w[1] = make_float4(q.d.y, q.d.z, q.tmin, q.tmax);
+    w[2] = make_float4(__int_as_float(q.self), __int_as_float(q.back), __int_as_float(q.win), __uint_as_float(fl));
+    w[3] = make_float4(q.mask.r, q.mask.g, q.mask.b, __int_as_float(top));
+}
+
+// the result fields only (trace -> shade)
+__device__ __forceinline__ void ray_store_result(RayRec &r, const Query &q) {
+    float4 *w = reinterpret_cast<float4 *>(&r);
+    unsigned fl = (q.closest ? 1u : 0u) | (q.unb ? 2u : 0u) | (q.skipchk ? 4u : 0u) | (q.skipped ? 8u : 0u);
+    w[1].w = q.tmax;
+    reinterpret_cast<int *>(&r)[10] = q.win;
+    reinterpret_cast<unsigned *>(&r)[11] = fl;
+    r.mask[0] = q.mask.r;
+    r.mask[1] = q.mask.g;
+    r.mask[2] = q.mask.b;
+}
+
+// wave sum of a counter, one atomic per wave
+__device__ __forceinline__ void wave_add(unsigned long long *dst, unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
+}
+
+__device__ __forceinline__ void flush_counters(const Params &p, const Counters &c) {
+    unsigned long long *st = p.stats;
+    wave_add(&st[0], c.prim);
+    wave_add(&st[1], c.shadow);
+    wave_add(&st[2], c.refr);
+    wave_add(&st[3], c.refl);
+    wave_add(&st[4], c.skip);
+    wave_add(&st[5], c.ub);
+    wave_add(&st[6], c.boxes);
+    wave_add(&st[7], c.ftests);
+    wave_add(&st[8], c.stests);
+}
+
+__global__ void __launch_bounds__(kBlock) wf_spawn(Params p) {
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const V3 ul = {p.ul[0], p.ul[1], p.ul[2]}, dh = {p.dh[0], p.dh[1], p.dh[2]}, dv = {p.dv[0], p.dv[1], p.dv[2]};
+    const V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
+    for (unsigned base = blockIdx.x * kBlock; base < p.total; base += gridDim.x * kBlock) {
+        unsigned i = base + threadIdx.x;
+        if (i < p.total) {
+            int px, py;
+            pixel_xy(p, i, px, py);
+            V3 pt = vadd(vadd(ul, vmul(dh, (float)px)), vmul(dv, (float)(py + p.y0)));
+            Query q;
+            q.o = eye;
+            q.d = vnorm(vsub(pt, eye));
+            q.tmin = 0.0f;
+            q.tmax = kFltMax;
+            q.unb = false;
+            q.self = -1;
+            q.back = -1;
+            q.closest = true;
+            q.skipchk = false;
+            q.skipped = false;
+            q.win = -1;
+            q.mask = {1.0f, 1.0f, 1.0f};
+            ray_store(p.rays[i], q, -1);
+            cnt.prim++;
+        }
+    }
+    flush_counters(p, cnt);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) wf_trace(Params p) {
+    extern __shared__ float4 lds[];
+    int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;
+    const unsigned n = *p.cin;
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (unsigned base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        unsigned i = base + threadIdx.x;
+        bool act = i < n;
+        int pix = 0;
+        Query q;
+        int top = 0;
+        if (act) {
+            pix = p.qin ? p.qin[i] : (int)i;
+            ray_load(p.rays[pix], q, top);
+        } else {
+            q.tmin = kInf;
+        }
+        if (MODE == MODE_BVH) {
+            q.bf = act && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+            if (act && !q.bf) bvh_trace(q, p, stk, cnt);
+            bool need = act && q.bf;
+            if (__ballot(need)) scan<false>(q, p, nullptr, nullptr, need, cnt.ftests, cnt.stests);
+        } else {
+            scan<false>(q, p, nullptr, nullptr, act, cnt.ftests, cnt.stests);
+        }
+        if (act) ray_store_result(p.rays[pix], q);
+    }
+    flush_counters(p, cnt);
+}
+
+template <int MAXF>
+__global__ void __launch_bounds__(kBlock) wf_shade(Params p) {
+    const unsigned n = *p.cin;
+    const int lane = threadIdx.x & 63;
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Frame<MAXF> *frames = reinterpret_cast<Frame<MAXF> *>(p.frames);
+    for (unsigned base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        unsigned i = base + threadIdx.x;
+        bool more = false;
+        int pix = 0;
+        if (i < n) {
+            pix = p.qin ? p.qin[i] : (int)i;
+            Query q;
+            int top;
+            ray_load(p.rays[pix], q, top);
+            C3 color;
+            more = advance<MAXF>(p, frames + (size_t)pix * MAXF, top, q, cnt, color);
+            if (more) {
+                ray_store(p.rays[pix], q, top);
+            } else {
+                int px, py;
+                pixel_xy(p, (unsigned)pix, px, py);
+                float *o = p.out + ((size_t)py * p.W + px) * 3;
+                o[0] = color.r;
+                o[1] = color.g;
+                o[2] = color.b;
+            }
+        }
+        // compaction of the follow-up rays: ballot + one atomic + mbcnt
+        unsigned long long m = __ballot(more);
+        if (m) {
+            int leader = __ffsll((long long)m) - 1;
+            unsigned b = 0;
+            if (lane == leader) b = atomicAdd(p.cout, (unsigned)__popcll(m));
+            b = __shfl(b, leader);
+            if (more) p.qout[b + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = pix;
+        }
+    }
+    flush_counters(p, cnt);
+}
+
 }  // namespace rt
 
 // ===========================================================================
@@ -942,6 +1135,7 @@ struct rt_scene {
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
+    long long opt_engine = -1;         // -1 auto, 0 megakernel, 1 wavefront
     long long opt_bvh_leaf = 8;        // SAH max leaf size
     long long opt_bvh_trav = 1000;     // SAH traversal cost, x1000 of a sphere test
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
@@ -959,6 +1153,13 @@ struct rt_scene {
     int *d_bkeys = nullptr;
     int bvh_depth = 0;
     int bvh_stack = 0;
+    // wavefront engine buffers (grown on demand)
+    RayRec *wf_rays = nullptr;
+    void *wf_frames = nullptr;
+    int *wf_q[2] = {nullptr, nullptr};
+    unsigned *wf_cnt = nullptr;        // 2 queue lengths
+    size_t wf_cap = 0, wf_frame_bytes = 0;
+    int last_iters = 0;
     bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
     bool last_valid = false;
@@ -1089,6 +1290,78 @@ int build_bvh(rt_scene *s, double D) {
     return RT_OK;
 }
 
+template <typename K>
+int persistent_grid(K kernel, size_t shm, int num_cu, unsigned work) {
+    int nb = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, shm);
+    long long g = (long long)std::max(1, nb) * num_cu;
+    long long need = ((long long)work + kBlock - 1) / kBlock;
+    return (int)std::max(1LL, std::min(g, need));
+}
+
+int wf_reserve(rt_scene *s, size_t px, size_t frame_bytes) {
+    if (px <= s->wf_cap && frame_bytes * px <= s->wf_frame_bytes) return RT_OK;
+    size_t cap = std::max(px, s->wf_cap);
+    if (s->wf_rays) (void)hipFree(s->wf_rays);
+    if (s->wf_frames) (void)hipFree(s->wf_frames);
+    for (int k = 0; k < 2; k++)
+        if (s->wf_q[k]) (void)hipFree(s->wf_q[k]);
+    s->wf_rays = nullptr;
+    s->wf_frames = nullptr;
+    s->wf_q[0] = s->wf_q[1] = nullptr;
+    s->wf_cap = s->wf_frame_bytes = 0;
+    if (hipMalloc(&s->wf_rays, cap * sizeof(RayRec)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&s->wf_frames, cap * frame_bytes) != hipSuccess) return RT_E_NOMEM;
+    for (int k = 0; k < 2; k++)
+        if (hipMalloc(&s->wf_q[k], cap * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
+    if (!s->wf_cnt && hipMalloc(&s->wf_cnt, 4 * sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
+    s->wf_cap = cap;
+    s->wf_frame_bytes = cap * frame_bytes;
+    return RT_OK;
+}
+
+// Wavefront render: spawn, then (trace, shade) until no pixel needs a ray.
+// Iterations run in batches; after each batch the remaining queue length is
+// read back, so the loop ends after (longest pixel's ray count) iterations.
+template <int MAXF>
+int launch_wavefront(rt_scene *s, Params p, int mode, hipStream_t st) {
+    int rc = wf_reserve(s, p.total, sizeof(Frame<MAXF>) * MAXF);
+    if (rc) return rc;
+    p.rays = s->wf_rays;
+    p.frames = s->wf_frames;
+    const size_t shm = mode == MODE_BVH ? (size_t)std::max(1, s->bvh_stack) * kBlock * sizeof(int) : 0;
+    unsigned total = p.total;
+    int g_spawn = persistent_grid(wf_spawn, 0, s->num_cu, total);
+    hipLaunchKernelGGL(wf_spawn, dim3(g_spawn), dim3(kBlock), 0, st, p);
+    if (hipMemcpyAsync(s->wf_cnt, &total, sizeof(unsigned), hipMemcpyHostToDevice, st) != hipSuccess) return RT_E_HIP;
+    auto trace_k = mode == MODE_BVH ? wf_trace<MODE_BVH> : wf_trace<MODE_SCAN>;
+    int g_trace = persistent_grid(trace_k, shm, s->num_cu, total);
+    int g_shade = persistent_grid(wf_shade<MAXF>, 0, s->num_cu, total);
+    // upper bound on one pixel's TraceRay calls: primary + (lights + 2) per node
+    long long nodes = (1LL << (std::min(p.depth, 20) + 1)) - 1;
+    long long bound = 1 + (long long)(p.nl + 2) * nodes;
+    const int batch = 8;
+    int it = 0;
+    unsigned h_left = total;
+    while (it < bound && h_left > 0) {
+        for (int b = 0; b < batch && it < bound; b++, it++) {
+            int cur = it & 1;
+            p.qin = it == 0 ? nullptr : s->wf_q[cur];
+            p.qout = s->wf_q[cur ^ 1];
+            p.cin = s->wf_cnt + cur;
+            p.cout = s->wf_cnt + (cur ^ 1);
+            hipLaunchKernelGGL(trace_k, dim3(g_trace), dim3(kBlock), shm, st, p);
+            if (hipMemsetAsync(s->wf_cnt + (cur ^ 1), 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
+            hipLaunchKernelGGL(wf_shade<MAXF>, dim3(g_shade), dim3(kBlock), 0, st, p);
+        }
+        if (hipMemcpyAsync(&h_left, s->wf_cnt + (it & 1), sizeof(unsigned), hipMemcpyDeviceToHost, st) != hipSuccess)
+            return RT_E_HIP;
+        if (hipStreamSynchronize(st) != hipSuccess) return RT_E_HIP;
+    }
+    s->last_iters = it;
+    return hipGetLastError() == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
 int launch(rt_scene *s, Params &p, hipStream_t st) {
     int depth = p.depth < 0 ? 0 : p.depth;
     if (depth > 16) return RT_E_UNSUPPORTED;
@@ -1111,6 +1384,13 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
         bool lds = s->opt_lds == 1 || (s->opt_lds == -1 && s->lds_bytes <= 64 * 1024);
         if (s->lds_bytes > 64 * 1024) lds = false;
         if (lds) mode = MODE_SCAN_LDS;
+    }
+    bool wavefront = s->opt_engine == 1 || (s->opt_engine == -1 && mode == MODE_BVH);
+    if (wavefront) {
+        int wmode = mode == MODE_BVH ? MODE_BVH : MODE_SCAN;
+        if (depth <= 4) return launch_wavefront<5>(s, p, wmode, st);
+        if (depth <= 8) return launch_wavefront<9>(s, p, wmode, st);
+        return launch_wavefront<17>(s, p, wmode, st);
     }
     hipError_t e;
     if (depth <= 4) e = launch_mode<5>(s, p, mode, st);
@@ -1306,6 +1586,11 @@ int rt_scene_destroy(rt_scene *s) {
     for (void *d : s->allocs) (void)hipFree(d);
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_bkeys) (void)hipFree(s->d_bkeys);
+    if (s->wf_rays) (void)hipFree(s->wf_rays);
+    if (s->wf_frames) (void)hipFree(s->wf_frames);
+    for (int k = 0; k < 2; k++)
+        if (s->wf_q[k]) (void)hipFree(s->wf_q[k]);
+    if (s->wf_cnt) (void)hipFree(s->wf_cnt);
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);
@@ -1323,6 +1608,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
+    else if (k == "engine") s->opt_engine = value;
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);
