@@ -153,6 +153,8 @@ struct Params {
     int *qout;
     const unsigned *cin;                 // queue lengths
     unsigned *cout;
+    int *spix;                           // [pool] pixel index owned by each path slot
+    unsigned pool;                       // path slots (<= total)
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -432,18 +434,45 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
 // ---------------------------------------------------------------------------
 // ShadeRay as a per-lane state machine
 // ---------------------------------------------------------------------------
-enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4 };
+enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4, PH_DONE = 5 };
 
+// One ShadeRay activation.  128 B for depth <= 4 (MAXF = 5): loaded and
+// stored whole (full cache lines) by advance(); the medium stack is only
+// indexed with compile-time indices so a frame copy stays in registers.
 template <int MAXF>
-struct Frame {
-    int obj, state, depth, phase, light, sn;
-    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
+struct alignas(16) Frame {
+    int obj;
+    unsigned state : 1, depth : 5, phase : 3, sn : 7, light : 16;
     float ei, et;                    // incidence / transmission refraction index
     V3 P, N, I;                      // hit point, shading normal (flipped for spheres), I = -ray
     float cosI;
     C3 dif, mask, acc;               // diffuse, cumulative shadow mask, running colour
     float Ft;                        // transmission Fresnel F (main.cpp:966)
+    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
 };
+static_assert(sizeof(Frame<5>) == 128, "frame layout");
+
+// medium-stack operations with static indices only (src/utility.h:6-12 objectInStack)
+template <int MAXF>
+__device__ __forceinline__ int stack_back(const Frame<MAXF> &f) {
+    int b = -1;
+#pragma unroll
+    for (int k = 0; k < MAXF; k++) b = ((int)f.sn - 1 == k) ? f.stack[k] : b;
+    return b;
+}
+template <int MAXF>
+__device__ __forceinline__ void stack_push(Frame<MAXF> &f, int v) {
+#pragma unroll
+    for (int k = 0; k < MAXF; k++) f.stack[k] = ((int)f.sn == k) ? v : f.stack[k];
+    f.sn = f.sn + 1;
+}
+template <int MAXF>
+__device__ __forceinline__ bool stack_has(const Frame<MAXF> &f, int obj) {
+    bool in = false;
+#pragma unroll
+    for (int k = 0; k < MAXF; k++) in |= (k < (int)f.sn) & (f.stack[k] == obj);
+    return in;
+}
 
 
 // Hit record of the winning intersection, recomputed exactly as TraceRay did.
@@ -553,93 +582,86 @@ __device__ __forceinline__ float schlick(float F0, float cosI) {
     return (float)((double)F0 + (1.0 - (double)F0) * (double)p5);
 }
 
-template <int MAXF>
-__device__ __forceinline__ bool in_stack(const Frame<MAXF> &f, int obj) {
-    bool in = false;
-    for (int q = 0; q < f.sn; q++) in |= (f.stack[q] == obj);
-    return in;
-}
-
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
+// c starts as a copy of the parent's stack (the reference copies the vector).
 template <int MAXF>
 __device__ void refr_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit, Counters &cnt) {
-    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
-    int n = f.sn;
+#pragma unroll
+    for (int k = 0; k < MAXF; k++) c.stack[k] = f.stack[k];
+    c.sn = f.sn;
     float hit_eta = p.objs[hit].eta;
     if (f.state == ENTERING) {
-        if (hit == f.obj) {
+        if (hit == (int)f.obj) {
             c.state = EXITING;
-            if (n > 0) {
-                c.ei = p.objs[c.stack[n - 1]].eta;
-                n--;
+            if (c.sn > 0) {
+                c.ei = p.objs[stack_back(c)].eta;
+                c.sn = c.sn - 1;
             } else {
                 c.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
                 cnt.ub++;
             }
-            c.et = n > 0 ? p.objs[c.stack[n - 1]].eta : p.eta_bkg;
-            if (n > 0) n--;
+            c.et = c.sn > 0 ? p.objs[stack_back(c)].eta : p.eta_bkg;
+            if (c.sn > 0) c.sn = c.sn - 1;
         } else {
             c.state = ENTERING;
             c.ei = f.et;
             c.et = hit_eta;
-            c.stack[n++] = hit;
+            stack_push(c, hit);
         }
-    } else if (n > 0) {
-        if (!in_stack(f, hit)) {
+    } else if (c.sn > 0) {
+        if (!stack_has(f, hit)) {
             c.state = ENTERING;
             c.ei = f.et;
             c.et = hit_eta;
-            c.stack[n++] = hit;
+            stack_push(c, hit);
         } else {
             c.state = EXITING;
             c.ei = f.et;
-            c.et = p.objs[c.stack[n - 1]].eta;
-            n--;
+            c.et = p.objs[stack_back(c)].eta;
+            c.sn = c.sn - 1;
         }
     } else {
         c.state = ENTERING;
         c.ei = p.eta_bkg;
         c.et = hit_eta;
-        c.stack[0] = hit;
-        n = 1;
+        c.sn = 0;
+        stack_push(c, hit);
     }
-    c.sn = n;
 }
 
 // Medium-stack transition for the reflection child (main.cpp:1134-1182).
 template <int MAXF>
 __device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit) {
-    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
-    int n = f.sn;
+#pragma unroll
+    for (int k = 0; k < MAXF; k++) c.stack[k] = f.stack[k];
+    c.sn = f.sn;
     float hit_eta = p.objs[hit].eta;
+    c.ei = f.ei;
     if (f.state == ENTERING) {
         c.state = ENTERING;
-        c.ei = f.ei;
-        if (n > 0) {
-            if (!in_stack(f, hit)) {
+        if (c.sn > 0) {
+            if (!stack_has(f, hit)) {
                 c.et = hit_eta;
-                c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
+                stack_push(c, (int)f.obj);   // pushes the incidence object, as the reference does
             } else {
-                c.et = p.objs[c.stack[n - 1]].eta;
-                n--;
+                c.et = p.objs[stack_back(c)].eta;
+                c.sn = c.sn - 1;
             }
         } else {
             c.et = hit_eta;
-            c.stack[0] = hit;
-            n = 1;
+            c.sn = 0;
+            stack_push(c, hit);
         }
     } else {
-        c.ei = f.ei;
-        if (hit == f.obj) {
+        if (hit == (int)f.obj) {
             c.state = EXITING;
             c.et = f.et;
         } else {
             c.state = ENTERING;
             c.et = hit_eta;
-            c.stack[n++] = hit;
+            stack_push(c, hit);
         }
     }
-    c.sn = n;
 }
 
 // Lane state between scans.
@@ -653,28 +675,44 @@ struct LaneState {
 // until the next TraceRay (returns true with q set up) or until the pixel is
 // done (returns false with `color` set).
 template <int MAXF>
+__device__ __forceinline__ void begin_child(const Params &p, Frame<MAXF> &f, Frame<MAXF> &c, const Query &q,
+                                            unsigned parent_phase) {
+    c.obj = q.win;
+    c.depth = f.depth - 1;
+    f.phase = parent_phase;
+    node_begin(p, c, q.o, q.d, q.tmax);
+}
+
+// Advance one pixel's ShadeRay state machine after its TraceRay: consume the
+// result, then run until the next TraceRay (returns true, q set up) or until
+// the pixel's colour is known (returns false, `color` set).  `fr` holds the
+// pixel's MAXF frames (scratch in the megakernel, HBM in the wavefront
+// engine); the current frame is worked on in registers and written back whole.
+template <int MAXF>
 __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &top_ref, Query &q, Counters &cnt,
                                         C3 &color) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
     int top = top_ref;
+    Frame<MAXF> f;
     // ---- consume the scan result ----
     if (top < 0) {                                   // primary (main.cpp:729-758)
         if (q.win < 0) {
             color = bkg;
             return false;
         }
-        Frame<MAXF> &f = fr[0];
         f.obj = q.win;
         f.ei = p.eta_bkg;
         f.et = p.objs[q.win].eta;
-        f.sn = 1;
-        f.stack[0] = q.win;
+        f.sn = 0;
+#pragma unroll
+        for (int k = 0; k < MAXF; k++) f.stack[k] = 0;
+        stack_push(f, q.win);
         f.state = ENTERING;
         f.depth = p.depth;
         node_begin(p, f, q.o, q.d, q.tmax);
         top = 0;
     } else {
-        Frame<MAXF> &f = fr[top];
+        f = fr[top];
         if (f.phase == PH_LIGHT) {                   // main.cpp:952-958
             f.mask = q.mask;
             const LightK &lt = p.lights[f.light];
@@ -688,19 +726,18 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
             C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), powf(max0(vdot(f.N, H)), ob.n));
             C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
             f.acc = cadd(f.acc, cmulc(cmulc(lc, f.mask), cadd(dc, sc)));
-            f.light++;
+            f.light = f.light + 1;
         } else if (f.phase == PH_REFR) {
             const ObjK &ob = p.objs[f.obj];
             if (q.skipped) {
                 cnt.skip++;                          // tmp_transparency stays 0
                 f.phase = PH_REFL;
             } else if (q.win >= 0) {
-                Frame<MAXF> &c = fr[top + 1];
+                Frame<MAXF> c;
                 refr_transition(p, f, c, q.win, cnt);
-                c.obj = q.win;
-                c.depth = f.depth - 1;
-                f.phase = PH_REFR_CHILD;
-                node_begin(p, c, q.o, q.d, q.tmax);
+                begin_child(p, f, c, q, PH_REFR_CHILD);
+                fr[top] = f;
+                f = c;
                 top++;
             } else {
                 C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)ob.opacity));
@@ -709,12 +746,11 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
             }
         } else if (f.phase == PH_REFL) {
             if (q.win >= 0) {
-                Frame<MAXF> &c = fr[top + 1];
+                Frame<MAXF> c;
                 refl_transition(p, f, c, q.win);
-                c.obj = q.win;
-                c.depth = f.depth - 1;
-                f.phase = PH_REFL_CHILD;
-                node_begin(p, c, q.o, q.d, q.tmax);
+                begin_child(p, f, c, q, PH_REFL_CHILD);
+                fr[top] = f;
+                f = c;
                 top++;
             } else {
                 // miss: refl = bkg * F_r; finish this node below
@@ -722,16 +758,15 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 float F0 = (ob.eta - 1) / (ob.eta + 1);
                 float Fr = schlick(F0 * F0, f.cosI);
                 f.acc = cadd(f.acc, cmulf(bkg, Fr));
-                f.phase = PH_REFL_CHILD + 1;         // done
+                f.phase = PH_DONE;
             }
         }
     }
     // ---- run the current frame forward ----
     for (;;) {
-        Frame<MAXF> &f = fr[top];
         const ObjK &ob = p.objs[f.obj];
         if (f.phase == PH_LIGHT) {
-            if (f.light < p.nl) {                    // shadow ray for light f.light
+            if ((int)f.light < p.nl) {               // shadow ray for light f.light
                 V3 L, sd;
                 float dl;
                 bool unb;
@@ -748,6 +783,7 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 q.win = -1;
                 q.mask = f.mask;
                 cnt.shadow++;
+                fr[top] = f;
                 top_ref = top;
                 return true;
             }
@@ -770,11 +806,12 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 q.self = -1;
                 q.closest = true;
                 q.skipchk = (f.sn > 0) && !ob.is_sphere;
-                q.back = f.sn > 0 ? f.stack[f.sn - 1] : -1;
+                q.back = stack_back(f);
                 q.skipped = false;
                 q.win = -1;
                 cnt.refr++;
                 f.phase = PH_REFR;
+                fr[top] = f;
                 top_ref = top;
                 return true;
             }
@@ -796,10 +833,11 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 q.skipped = false;
                 q.win = -1;
                 cnt.refl++;
+                fr[top] = f;
                 top_ref = top;
                 return true;
             }
-            f.phase = PH_REFL_CHILD + 1;
+            f.phase = PH_DONE;
         }
         // node complete: ((dka + spec) + trans) + refl already folded into acc
         C3 c = f.acc;
@@ -809,17 +847,17 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
             return false;
         }
         top--;
-        Frame<MAXF> &pf = fr[top];
-        const ObjK &pob = p.objs[pf.obj];
-        if (pf.phase == PH_REFR_CHILD) {             // main.cpp:1072-1083
-            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)pf.Ft)), (float)(1.0 - (double)pob.opacity));
-            pf.acc = cadd(pf.acc, tr);
-            pf.phase = PH_REFL;
+        f = fr[top];
+        const ObjK &pob = p.objs[f.obj];
+        if (f.phase == PH_REFR_CHILD) {              // main.cpp:1072-1083
+            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)pob.opacity));
+            f.acc = cadd(f.acc, tr);
+            f.phase = PH_REFL;
         } else {                                     // PH_REFL_CHILD, main.cpp:1184-1194
             float F0 = (pob.eta - 1) / (pob.eta + 1);
-            float Fr = schlick(F0 * F0, pf.cosI);
-            pf.acc = cadd(pf.acc, cmulf(c, Fr));
-            pf.phase = PH_REFL_CHILD + 1;
+            float Fr = schlick(F0 * F0, f.cosI);
+            f.acc = cadd(f.acc, cmulf(c, Fr));
+            f.phase = PH_DONE;
         }
     }
 }
@@ -1011,30 +1049,37 @@ __device__ __forceinline__ void flush_counters(const Params &p, const Counters &
     wave_add(&st[8], c.stests);
 }
 
-__global__ void __launch_bounds__(kBlock) wf_spawn(Params p) {
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+// primary ray of pixel `idx` (main.cpp:720-729) into path slot `slot`
+__device__ __forceinline__ void spawn_primary(const Params &p, unsigned idx, int slot) {
+    int px, py;
+    pixel_xy(p, idx, px, py);
     const V3 ul = {p.ul[0], p.ul[1], p.ul[2]}, dh = {p.dh[0], p.dh[1], p.dh[2]}, dv = {p.dv[0], p.dv[1], p.dv[2]};
     const V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
-    for (unsigned base = blockIdx.x * kBlock; base < p.total; base += gridDim.x * kBlock) {
+    V3 pt = vadd(vadd(ul, vmul(dh, (float)px)), vmul(dv, (float)(py + p.y0)));
+    Query q;
+    q.o = eye;
+    q.d = vnorm(vsub(pt, eye));
+    q.tmin = 0.0f;                     // primary rays accept any t > 0 (main.cpp:736)
+    q.tmax = kFltMax;
+    q.unb = false;
+    q.self = -1;
+    q.back = -1;
+    q.closest = true;
+    q.skipchk = false;
+    q.skipped = false;
+    q.win = -1;
+    q.mask = {1.0f, 1.0f, 1.0f};
+    ray_store(p.rays[slot], q, -1);
+    p.spix[slot] = (int)idx;
+}
+
+// fill every path slot with the first `pool` pixels
+__global__ void __launch_bounds__(kBlock) wf_spawn(Params p) {
+    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (unsigned base = blockIdx.x * kBlock; base < p.pool; base += gridDim.x * kBlock) {
         unsigned i = base + threadIdx.x;
-        if (i < p.total) {
-            int px, py;
-            pixel_xy(p, i, px, py);
-            V3 pt = vadd(vadd(ul, vmul(dh, (float)px)), vmul(dv, (float)(py + p.y0)));
-            Query q;
-            q.o = eye;
-            q.d = vnorm(vsub(pt, eye));
-            q.tmin = 0.0f;
-            q.tmax = kFltMax;
-            q.unb = false;
-            q.self = -1;
-            q.back = -1;
-            q.closest = true;
-            q.skipchk = false;
-            q.skipped = false;
-            q.win = -1;
-            q.mask = {1.0f, 1.0f, 1.0f};
-            ray_store(p.rays[i], q, -1);
+        if (i < p.pool) {
+            spawn_primary(p, i, (int)i);
             cnt.prim++;
         }
     }
@@ -1080,8 +1125,8 @@ __global__ void __launch_bounds__(kBlock) wf_shade(Params p) {
     Frame<MAXF> *frames = reinterpret_cast<Frame<MAXF> *>(p.frames);
     for (unsigned base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
         unsigned i = base + threadIdx.x;
-        bool more = false;
-        int pix = 0;
+        bool more = false, done = false;
+        int pix = 0;                                 // path slot
         if (i < n) {
             pix = p.qin ? p.qin[i] : (int)i;
             Query q;
@@ -1093,11 +1138,28 @@ __global__ void __launch_bounds__(kBlock) wf_shade(Params p) {
                 ray_store(p.rays[pix], q, top);
             } else {
                 int px, py;
-                pixel_xy(p, (unsigned)pix, px, py);
+                pixel_xy(p, (unsigned)p.spix[pix], px, py);
                 float *o = p.out + ((size_t)py * p.W + px) * 3;
                 o[0] = color.r;
                 o[1] = color.g;
                 o[2] = color.b;
+                done = true;
+            }
+        }
+        // refill finished slots with new pixels: ballot + one atomic + mbcnt
+        unsigned long long dm = __ballot(done);
+        if (dm) {
+            int leader = __ffsll((long long)dm) - 1;
+            unsigned b = 0;
+            if (lane == leader) b = atomicAdd(p.work, (unsigned)__popcll(dm));
+            b = __shfl(b, leader);
+            if (done) {
+                unsigned idx = b + (unsigned)__popcll(dm & ((1ull << lane) - 1ull));
+                if (idx < p.total) {
+                    spawn_primary(p, idx, pix);
+                    cnt.prim++;
+                    more = true;
+                }
             }
         }
         // compaction of the follow-up rays: ballot + one atomic + mbcnt
@@ -1155,6 +1217,8 @@ struct rt_scene {
     int bvh_stack = 0;
     // wavefront engine buffers (grown on demand)
     RayRec *wf_rays = nullptr;
+    int *wf_spix = nullptr;
+    long long opt_pool = 1 << 20;      // wavefront path slots
     void *wf_frames = nullptr;
     int *wf_q[2] = {nullptr, nullptr};
     unsigned *wf_cnt = nullptr;        // 2 queue lengths
@@ -1303,14 +1367,17 @@ int wf_reserve(rt_scene *s, size_t px, size_t frame_bytes) {
     if (px <= s->wf_cap && frame_bytes * px <= s->wf_frame_bytes) return RT_OK;
     size_t cap = std::max(px, s->wf_cap);
     if (s->wf_rays) (void)hipFree(s->wf_rays);
+    if (s->wf_spix) (void)hipFree(s->wf_spix);
     if (s->wf_frames) (void)hipFree(s->wf_frames);
     for (int k = 0; k < 2; k++)
         if (s->wf_q[k]) (void)hipFree(s->wf_q[k]);
     s->wf_rays = nullptr;
+    s->wf_spix = nullptr;
     s->wf_frames = nullptr;
     s->wf_q[0] = s->wf_q[1] = nullptr;
     s->wf_cap = s->wf_frame_bytes = 0;
     if (hipMalloc(&s->wf_rays, cap * sizeof(RayRec)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&s->wf_spix, cap * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
     if (hipMalloc(&s->wf_frames, cap * frame_bytes) != hipSuccess) return RT_E_NOMEM;
     for (int k = 0; k < 2; k++)
         if (hipMalloc(&s->wf_q[k], cap * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
@@ -1325,21 +1392,28 @@ int wf_reserve(rt_scene *s, size_t px, size_t frame_bytes) {
 // read back, so the loop ends after (longest pixel's ray count) iterations.
 template <int MAXF>
 int launch_wavefront(rt_scene *s, Params p, int mode, hipStream_t st) {
-    int rc = wf_reserve(s, p.total, sizeof(Frame<MAXF>) * MAXF);
+    unsigned total = p.total;
+    unsigned pool = (unsigned)std::max(1LL, std::min((long long)total, s->opt_pool));
+    int rc = wf_reserve(s, pool, sizeof(Frame<MAXF>) * MAXF);
     if (rc) return rc;
     p.rays = s->wf_rays;
     p.frames = s->wf_frames;
+    p.spix = s->wf_spix;
+    p.pool = pool;
     const size_t shm = mode == MODE_BVH ? (size_t)std::max(1, s->bvh_stack) * kBlock * sizeof(int) : 0;
-    unsigned total = p.total;
-    int g_spawn = persistent_grid(wf_spawn, 0, s->num_cu, total);
+    // the pool takes pixels [0, pool); refills continue from the work counter
+    if (hipMemsetD32Async((hipDeviceptr_t)s->work, (int)pool, 1, st) != hipSuccess) return RT_E_HIP;
+    int g_spawn = persistent_grid(wf_spawn, 0, s->num_cu, pool);
     hipLaunchKernelGGL(wf_spawn, dim3(g_spawn), dim3(kBlock), 0, st, p);
-    if (hipMemcpyAsync(s->wf_cnt, &total, sizeof(unsigned), hipMemcpyHostToDevice, st) != hipSuccess) return RT_E_HIP;
+    if (hipMemsetD32Async((hipDeviceptr_t)s->wf_cnt, (int)pool, 1, st) != hipSuccess) return RT_E_HIP;
     auto trace_k = mode == MODE_BVH ? wf_trace<MODE_BVH> : wf_trace<MODE_SCAN>;
-    int g_trace = persistent_grid(trace_k, shm, s->num_cu, total);
-    int g_shade = persistent_grid(wf_shade<MAXF>, 0, s->num_cu, total);
-    // upper bound on one pixel's TraceRay calls: primary + (lights + 2) per node
+    int g_trace = persistent_grid(trace_k, shm, s->num_cu, pool);
+    int g_shade = persistent_grid(wf_shade<MAXF>, 0, s->num_cu, pool);
+    // upper bound on iterations: every pixel's TraceRay calls, one per iteration
+    // per slot (primary + (lights + 2) per node), pixels streamed through the pool
     long long nodes = (1LL << (std::min(p.depth, 20) + 1)) - 1;
-    long long bound = 1 + (long long)(p.nl + 2) * nodes;
+    long long per_px = 1 + (long long)(p.nl + 2) * nodes;
+    long long bound = per_px * (((long long)total + pool - 1) / pool) + per_px;
     const int batch = 8;
     int it = 0;
     unsigned h_left = total;
@@ -1587,6 +1661,7 @@ int rt_scene_destroy(rt_scene *s) {
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_bkeys) (void)hipFree(s->d_bkeys);
     if (s->wf_rays) (void)hipFree(s->wf_rays);
+    if (s->wf_spix) (void)hipFree(s->wf_spix);
     if (s->wf_frames) (void)hipFree(s->wf_frames);
     for (int k = 0; k < 2; k++)
         if (s->wf_q[k]) (void)hipFree(s->wf_q[k]);
@@ -1609,6 +1684,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
     else if (k == "engine") s->opt_engine = value;
+    else if (k == "pool") s->opt_pool = std::max(64LL, value);
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);

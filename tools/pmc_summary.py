@@ -10,21 +10,24 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 base = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "render_kernel"
 vals, disp = {}, {}
 for f in sorted(glob.glob(os.path.join(base, "p*", "run_counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
-        if "render_kernel" not in row["Kernel_Name"]:
+        if KERNEL not in row["Kernel_Name"]:
             continue
         name = row["Counter_Name"]
         vals[name] = vals.get(name, 0.0) + float(row["Counter_Value"])
         disp.setdefault(name, set()).add(row["Dispatch_Id"])
-per = {k: v / len(disp[k]) for k, v in vals.items()}
+# per render: sum over all dispatches of the kernel / number of renders
+renders = int(os.environ.get("RENDERS", "1"))
+per = {k: v / renders for k, v in vals.items()}
 dur = []
 for f in sorted(glob.glob(os.path.join(base, "p*", "run_kernel_trace.csv"))):
     for row in csv.DictReader(open(f)):
-        if "render_kernel" in row["Kernel_Name"]:
+        if KERNEL in row["Kernel_Name"]:
             dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-out = {"per_launch": per, "kernel_ns_mean": sum(dur) / max(1, len(dur)), "launches": len(dur)}
+out = {"kernel": KERNEL, "per_render": per, "kernel_ns_per_render": sum(dur) / renders, "dispatches": len(dur)}
 g = lambda k: per.get(k, float("nan"))
 d = {}
 d["valu_inst_per_wave"] = g("SQ_INSTS_VALU") / g("SQ_WAVES")
