@@ -146,20 +146,11 @@ struct Params {
     const int *__restrict__ bkeys;
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
-    // wavefront engine (engine = 1)
-    struct RayRec *rays;                 // [pixels] the pixel's in-flight ray + frame index
-    void *frames;                        // [pixels][MAXF] Frame<MAXF> (ShadeRay frames in HBM)
-    const int *qin;                      // ray queue (pixel indices), NULL = identity
-    int *qout;
-    const unsigned *cin;                 // queue lengths
-    unsigned *cout;
-    int *spix;                           // [pool] pixel index owned by each path slot
-    unsigned pool;                       // path slots (<= total)
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 #ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 3                   // waves per SIMD the register budget must allow
+#define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif
 constexpr int kStack = 40;               // max per-lane BVH stack entries; LDS holds the tree's bound
 constexpr int kBlock = 256;
@@ -240,10 +231,10 @@ __device__ __forceinline__ bool sphere_test(float4 s, V3 o, V3 d, float &t1, flo
 // arrays were staged into LDS (lds_f, lds_s); otherwise scalar loads.
 template <bool SRC_LDS>
 __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s,
-                                     bool part, unsigned long long &ft, unsigned long long &st) {
+                                     bool part, unsigned &ft, unsigned &st) {
     if (!part) return;
-    ft += (unsigned long long)p.nf;
-    st += (unsigned long long)p.ns;
+    ft += (unsigned)p.nf;
+    st += (unsigned)p.ns;
     for (int i = 0; i < p.nf; i++) {
         float4 f0, f1, f2, f3, f4;
         if (SRC_LDS) {
@@ -284,10 +275,14 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 // rays against spheres, > kHits semi-transparent shadow hits) set q.bf and are
 // re-run by the brute-force scan.
 // ---------------------------------------------------------------------------
+// Per-lane counters kept small (VGPR pressure): ray kinds are counted per
+// wave with ballots in the main loop (scalar registers); only the rare events
+// and the executed-test counts stay per lane.
 struct Counters {
-    unsigned prim, shadow, refr, refl, skip, ub;
-    unsigned long long boxes, ftests, stests;   // ray-box, ray-face, ray-sphere tests executed
+    unsigned skip, ub;
+    unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
 };
+enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
 constexpr int kHits = 8;
 
@@ -304,15 +299,15 @@ __device__ __forceinline__ void slab(float lx, float ly, float lz, float hx, flo
     tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
 }
 
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
+// stk: this lane's stack (entries kBlock apart); hits: its kHits-entry list of
+// shadow-hit object keys (also kBlock apart), both in LDS.
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
     const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
     int win = -1;
     int nh = 0;
-    int hkey[kHits];
-    float hf[kHits];
     bool opaque = false;
     int sp = 0;
     int node = 0;
@@ -389,8 +384,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
                         if (f == 0.0f && p.shadow_early_out) {
                             opaque = true;
                         } else if (nh < kHits) {
-                            hkey[nh] = key;
-                            hf[nh] = f;
+                            hits[nh * kBlock] = key;
                             nh++;
                         } else {
                             q.bf = true;           // too many: let the scan redo it in order
@@ -413,20 +407,17 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
         if (opaque) {
             q.mask = {0.0f, 0.0f, 0.0f};
         } else {
-            // multiply in object order (insertion sort; nh <= kHits)
+            // multiply in object order (insertion sort of the LDS list; nh <= kHits)
             for (int i = 1; i < nh; i++) {
-                int k = hkey[i];
-                float f = hf[i];
+                int k = hits[i * kBlock];
                 int j = i - 1;
-                while (j >= 0 && hkey[j] > k) {
-                    hkey[j + 1] = hkey[j];
-                    hf[j + 1] = hf[j];
+                while (j >= 0 && hits[j * kBlock] > k) {
+                    hits[(j + 1) * kBlock] = hits[j * kBlock];
                     j--;
                 }
-                hkey[j + 1] = k;
-                hf[j + 1] = f;
+                hits[(j + 1) * kBlock] = k;
             }
-            for (int i = 0; i < nh; i++) q.mask = cmulf(q.mask, hf[i]);
+            for (int i = 0; i < nh; i++) q.mask = cmulf(q.mask, cst(p.ofac)[hits[i * kBlock]]);
         }
     }
 }
@@ -434,45 +425,18 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
 // ---------------------------------------------------------------------------
 // ShadeRay as a per-lane state machine
 // ---------------------------------------------------------------------------
-enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4, PH_DONE = 5 };
+enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4 };
 
-// One ShadeRay activation.  128 B for depth <= 4 (MAXF = 5): loaded and
-// stored whole (full cache lines) by advance(); the medium stack is only
-// indexed with compile-time indices so a frame copy stays in registers.
 template <int MAXF>
-struct alignas(16) Frame {
-    int obj;
-    unsigned state : 1, depth : 5, phase : 3, sn : 7, light : 16;
+struct Frame {
+    int obj, state, depth, phase, light, sn;
+    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
     float ei, et;                    // incidence / transmission refraction index
     V3 P, N, I;                      // hit point, shading normal (flipped for spheres), I = -ray
     float cosI;
     C3 dif, mask, acc;               // diffuse, cumulative shadow mask, running colour
     float Ft;                        // transmission Fresnel F (main.cpp:966)
-    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
 };
-static_assert(sizeof(Frame<5>) == 128, "frame layout");
-
-// medium-stack operations with static indices only (src/utility.h:6-12 objectInStack)
-template <int MAXF>
-__device__ __forceinline__ int stack_back(const Frame<MAXF> &f) {
-    int b = -1;
-#pragma unroll
-    for (int k = 0; k < MAXF; k++) b = ((int)f.sn - 1 == k) ? f.stack[k] : b;
-    return b;
-}
-template <int MAXF>
-__device__ __forceinline__ void stack_push(Frame<MAXF> &f, int v) {
-#pragma unroll
-    for (int k = 0; k < MAXF; k++) f.stack[k] = ((int)f.sn == k) ? v : f.stack[k];
-    f.sn = f.sn + 1;
-}
-template <int MAXF>
-__device__ __forceinline__ bool stack_has(const Frame<MAXF> &f, int obj) {
-    bool in = false;
-#pragma unroll
-    for (int k = 0; k < MAXF; k++) in |= (k < (int)f.sn) & (f.stack[k] == obj);
-    return in;
-}
 
 
 // Hit record of the winning intersection, recomputed exactly as TraceRay did.
@@ -582,86 +546,93 @@ __device__ __forceinline__ float schlick(float F0, float cosI) {
     return (float)((double)F0 + (1.0 - (double)F0) * (double)p5);
 }
 
+template <int MAXF>
+__device__ __forceinline__ bool in_stack(const Frame<MAXF> &f, int obj) {
+    bool in = false;
+    for (int q = 0; q < f.sn; q++) in |= (f.stack[q] == obj);
+    return in;
+}
+
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
-// c starts as a copy of the parent's stack (the reference copies the vector).
 template <int MAXF>
 __device__ void refr_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit, Counters &cnt) {
-#pragma unroll
-    for (int k = 0; k < MAXF; k++) c.stack[k] = f.stack[k];
-    c.sn = f.sn;
+    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
+    int n = f.sn;
     float hit_eta = p.objs[hit].eta;
     if (f.state == ENTERING) {
-        if (hit == (int)f.obj) {
+        if (hit == f.obj) {
             c.state = EXITING;
-            if (c.sn > 0) {
-                c.ei = p.objs[stack_back(c)].eta;
-                c.sn = c.sn - 1;
+            if (n > 0) {
+                c.ei = p.objs[c.stack[n - 1]].eta;
+                n--;
             } else {
                 c.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
                 cnt.ub++;
             }
-            c.et = c.sn > 0 ? p.objs[stack_back(c)].eta : p.eta_bkg;
-            if (c.sn > 0) c.sn = c.sn - 1;
+            c.et = n > 0 ? p.objs[c.stack[n - 1]].eta : p.eta_bkg;
+            if (n > 0) n--;
         } else {
             c.state = ENTERING;
             c.ei = f.et;
             c.et = hit_eta;
-            stack_push(c, hit);
+            c.stack[n++] = hit;
         }
-    } else if (c.sn > 0) {
-        if (!stack_has(f, hit)) {
+    } else if (n > 0) {
+        if (!in_stack(f, hit)) {
             c.state = ENTERING;
             c.ei = f.et;
             c.et = hit_eta;
-            stack_push(c, hit);
+            c.stack[n++] = hit;
         } else {
             c.state = EXITING;
             c.ei = f.et;
-            c.et = p.objs[stack_back(c)].eta;
-            c.sn = c.sn - 1;
+            c.et = p.objs[c.stack[n - 1]].eta;
+            n--;
         }
     } else {
         c.state = ENTERING;
         c.ei = p.eta_bkg;
         c.et = hit_eta;
-        c.sn = 0;
-        stack_push(c, hit);
+        c.stack[0] = hit;
+        n = 1;
     }
+    c.sn = n;
 }
 
 // Medium-stack transition for the reflection child (main.cpp:1134-1182).
 template <int MAXF>
 __device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit) {
-#pragma unroll
-    for (int k = 0; k < MAXF; k++) c.stack[k] = f.stack[k];
-    c.sn = f.sn;
+    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
+    int n = f.sn;
     float hit_eta = p.objs[hit].eta;
-    c.ei = f.ei;
     if (f.state == ENTERING) {
         c.state = ENTERING;
-        if (c.sn > 0) {
-            if (!stack_has(f, hit)) {
+        c.ei = f.ei;
+        if (n > 0) {
+            if (!in_stack(f, hit)) {
                 c.et = hit_eta;
-                stack_push(c, (int)f.obj);   // pushes the incidence object, as the reference does
+                c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
             } else {
-                c.et = p.objs[stack_back(c)].eta;
-                c.sn = c.sn - 1;
+                c.et = p.objs[c.stack[n - 1]].eta;
+                n--;
             }
         } else {
             c.et = hit_eta;
-            c.sn = 0;
-            stack_push(c, hit);
+            c.stack[0] = hit;
+            n = 1;
         }
     } else {
-        if (hit == (int)f.obj) {
+        c.ei = f.ei;
+        if (hit == f.obj) {
             c.state = EXITING;
             c.et = f.et;
         } else {
             c.state = ENTERING;
             c.et = hit_eta;
-            stack_push(c, hit);
+            c.stack[n++] = hit;
         }
     }
+    c.sn = n;
 }
 
 // Lane state between scans.
@@ -674,45 +645,30 @@ struct LaneState {
 // Advance one lane after its scan: consume the result, run ShadeRay logic
 // until the next TraceRay (returns true with q set up) or until the pixel is
 // done (returns false with `color` set).
+// Returns the kind of the TraceRay it set up in q (RK_SHADOW/RK_REFR/RK_REFL),
+// or RK_NONE when the pixel is finished (`color` set).
 template <int MAXF>
-__device__ __forceinline__ void begin_child(const Params &p, Frame<MAXF> &f, Frame<MAXF> &c, const Query &q,
-                                            unsigned parent_phase) {
-    c.obj = q.win;
-    c.depth = f.depth - 1;
-    f.phase = parent_phase;
-    node_begin(p, c, q.o, q.d, q.tmax);
-}
-
-// Advance one pixel's ShadeRay state machine after its TraceRay: consume the
-// result, then run until the next TraceRay (returns true, q set up) or until
-// the pixel's colour is known (returns false, `color` set).  `fr` holds the
-// pixel's MAXF frames (scratch in the megakernel, HBM in the wavefront
-// engine); the current frame is worked on in registers and written back whole.
-template <int MAXF>
-__device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &top_ref, Query &q, Counters &cnt,
-                                        C3 &color) {
+__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
-    int top = top_ref;
-    Frame<MAXF> f;
+    int top = ls.top;
     // ---- consume the scan result ----
     if (top < 0) {                                   // primary (main.cpp:729-758)
         if (q.win < 0) {
             color = bkg;
-            return false;
+            return RK_NONE;
         }
+        Frame<MAXF> &f = ls.fr[0];
         f.obj = q.win;
         f.ei = p.eta_bkg;
         f.et = p.objs[q.win].eta;
-        f.sn = 0;
-#pragma unroll
-        for (int k = 0; k < MAXF; k++) f.stack[k] = 0;
-        stack_push(f, q.win);
+        f.sn = 1;
+        f.stack[0] = q.win;
         f.state = ENTERING;
         f.depth = p.depth;
         node_begin(p, f, q.o, q.d, q.tmax);
         top = 0;
     } else {
-        f = fr[top];
+        Frame<MAXF> &f = ls.fr[top];
         if (f.phase == PH_LIGHT) {                   // main.cpp:952-958
             f.mask = q.mask;
             const LightK &lt = p.lights[f.light];
@@ -726,18 +682,19 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
             C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), powf(max0(vdot(f.N, H)), ob.n));
             C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
             f.acc = cadd(f.acc, cmulc(cmulc(lc, f.mask), cadd(dc, sc)));
-            f.light = f.light + 1;
+            f.light++;
         } else if (f.phase == PH_REFR) {
             const ObjK &ob = p.objs[f.obj];
             if (q.skipped) {
                 cnt.skip++;                          // tmp_transparency stays 0
                 f.phase = PH_REFL;
             } else if (q.win >= 0) {
-                Frame<MAXF> c;
+                Frame<MAXF> &c = ls.fr[top + 1];
                 refr_transition(p, f, c, q.win, cnt);
-                begin_child(p, f, c, q, PH_REFR_CHILD);
-                fr[top] = f;
-                f = c;
+                c.obj = q.win;
+                c.depth = f.depth - 1;
+                f.phase = PH_REFR_CHILD;
+                node_begin(p, c, q.o, q.d, q.tmax);
                 top++;
             } else {
                 C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)ob.opacity));
@@ -746,11 +703,12 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
             }
         } else if (f.phase == PH_REFL) {
             if (q.win >= 0) {
-                Frame<MAXF> c;
+                Frame<MAXF> &c = ls.fr[top + 1];
                 refl_transition(p, f, c, q.win);
-                begin_child(p, f, c, q, PH_REFL_CHILD);
-                fr[top] = f;
-                f = c;
+                c.obj = q.win;
+                c.depth = f.depth - 1;
+                f.phase = PH_REFL_CHILD;
+                node_begin(p, c, q.o, q.d, q.tmax);
                 top++;
             } else {
                 // miss: refl = bkg * F_r; finish this node below
@@ -758,15 +716,16 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 float F0 = (ob.eta - 1) / (ob.eta + 1);
                 float Fr = schlick(F0 * F0, f.cosI);
                 f.acc = cadd(f.acc, cmulf(bkg, Fr));
-                f.phase = PH_DONE;
+                f.phase = PH_REFL_CHILD + 1;         // done
             }
         }
     }
     // ---- run the current frame forward ----
     for (;;) {
+        Frame<MAXF> &f = ls.fr[top];
         const ObjK &ob = p.objs[f.obj];
         if (f.phase == PH_LIGHT) {
-            if ((int)f.light < p.nl) {               // shadow ray for light f.light
+            if (f.light < p.nl) {                    // shadow ray for light f.light
                 V3 L, sd;
                 float dl;
                 bool unb;
@@ -782,10 +741,8 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 q.skipped = false;
                 q.win = -1;
                 q.mask = f.mask;
-                cnt.shadow++;
-                fr[top] = f;
-                top_ref = top;
-                return true;
+                ls.top = top;
+                return RK_SHADOW;
             }
             // ambient + specular sum, then Fresnel / transmission (main.cpp:961-992)
             f.acc = cadd(cmulf(f.dif, ob.ka), f.acc);
@@ -806,14 +763,12 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 q.self = -1;
                 q.closest = true;
                 q.skipchk = (f.sn > 0) && !ob.is_sphere;
-                q.back = stack_back(f);
+                q.back = f.sn > 0 ? f.stack[f.sn - 1] : -1;
                 q.skipped = false;
                 q.win = -1;
-                cnt.refr++;
                 f.phase = PH_REFR;
-                fr[top] = f;
-                top_ref = top;
-                return true;
+                ls.top = top;
+                return RK_REFR;
             }
             f.phase = PH_REFL;
         }
@@ -832,32 +787,30 @@ __device__ __forceinline__ bool advance(const Params &p, Frame<MAXF> *fr, int &t
                 q.skipchk = false;
                 q.skipped = false;
                 q.win = -1;
-                cnt.refl++;
-                fr[top] = f;
-                top_ref = top;
-                return true;
+                ls.top = top;
+                return RK_REFL;
             }
-            f.phase = PH_DONE;
+            f.phase = PH_REFL_CHILD + 1;
         }
         // node complete: ((dka + spec) + trans) + refl already folded into acc
         C3 c = f.acc;
         if (top == 0) {
             color = c;
-            top_ref = -1;
-            return false;
+            ls.top = -1;
+            return RK_NONE;
         }
         top--;
-        f = fr[top];
-        const ObjK &pob = p.objs[f.obj];
-        if (f.phase == PH_REFR_CHILD) {              // main.cpp:1072-1083
-            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)pob.opacity));
-            f.acc = cadd(f.acc, tr);
-            f.phase = PH_REFL;
+        Frame<MAXF> &pf = ls.fr[top];
+        const ObjK &pob = p.objs[pf.obj];
+        if (pf.phase == PH_REFR_CHILD) {             // main.cpp:1072-1083
+            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)pf.Ft)), (float)(1.0 - (double)pob.opacity));
+            pf.acc = cadd(pf.acc, tr);
+            pf.phase = PH_REFL;
         } else {                                     // PH_REFL_CHILD, main.cpp:1184-1194
             float F0 = (pob.eta - 1) / (pob.eta + 1);
-            float Fr = schlick(F0 * F0, f.cosI);
-            f.acc = cadd(f.acc, cmulf(c, Fr));
-            f.phase = PH_DONE;
+            float Fr = schlick(F0 * F0, pf.cosI);
+            pf.acc = cadd(pf.acc, cmulf(c, Fr));
+            pf.phase = PH_REFL_CHILD + 1;
         }
     }
 }
@@ -888,17 +841,21 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;   // MODE_BVH: stack[k * kBlock]
+    Counters cnt = {0, 0, 0, 0, 0};
+    unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
+    int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: hits[k * kBlock], k < kHits
+    int *stk = hits + kHits * kBlock;                       //           stack[k * kBlock]
     Query q;
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
     int px = 0, py = 0;
     for (;;) {
+        int kind = RK_NONE;
         if (pending) {
             C3 color;
-            pending = advance<MAXF>(p, ls.fr, ls.top, q, cnt, color);
+            kind = advance<MAXF>(p, ls, q, cnt, color);
+            pending = kind != RK_NONE;
             if (!pending) {
                 float *o = p.out + ((size_t)py * p.W + px) * 3;
                 o[0] = color.r;
@@ -936,7 +893,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                         q.skipped = false;
                         q.win = -1;
                         ls.top = -1;
-                        cnt.prim++;
+                        kind = RK_PRIMARY;
                         busy = true;
                         pending = true;
                     }
@@ -945,9 +902,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         }
         if (!pending) q.tmin = kInf;                 // lane sits this scan out
         if (__ballot(pending) == 0ull) break;
+        w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
+        w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
+        w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
+        w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         if (MODE == MODE_BVH) {
             q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
-            if (pending && !q.bf) bvh_trace(q, p, stk, cnt);
+            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
             bool need = pending && q.bf;
             if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
         } else {
@@ -955,224 +916,17 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         }
     }
     unsigned long long *st = p.stats;
-    atomicAdd(&st[0], (unsigned long long)cnt.prim);
-    atomicAdd(&st[1], (unsigned long long)cnt.shadow);
-    atomicAdd(&st[2], (unsigned long long)cnt.refr);
-    atomicAdd(&st[3], (unsigned long long)cnt.refl);
+    if (lane == 0) {
+        atomicAdd(&st[0], w_prim);
+        atomicAdd(&st[1], w_shadow);
+        atomicAdd(&st[2], w_refr);
+        atomicAdd(&st[3], w_refl);
+    }
     atomicAdd(&st[4], (unsigned long long)cnt.skip);
     atomicAdd(&st[5], (unsigned long long)cnt.ub);
-    atomicAdd(&st[6], cnt.boxes);
-    atomicAdd(&st[7], cnt.ftests);
-    atomicAdd(&st[8], cnt.stests);
-}
-
-
-// ===========================================================================
-// Wavefront engine: the same ShadeRay state machine, one ray per pixel in
-// flight, split into a lean trace kernel and a shade kernel per iteration.
-//   wf_spawn : primary ray of every pixel (main.cpp:720-729)         -> queue
-//   wf_trace : TraceRay for every queued ray (BVH or scan)
-//   wf_shade : consume the result, run ShadeRay to the pixel's next TraceRay
-//              and append it to the next queue (wave ballot + one atomicAdd
-//              + mbcnt prefix), or write the finished pixel
-// Per-pixel state lives in HBM: RayRec (64 B) + MAXF Frame records.
-// ===========================================================================
-struct RayRec {
-    float o[3], d[3];
-    float tmin, tmax;
-    int self, back, win;
-    unsigned flags;          // 1 closest, 2 unb, 4 skipchk, 8 skipped
-    float mask[3];
-    int top;                 // ShadeRay frame index, -1: primary pending
-};
-static_assert(sizeof(RayRec) == 64, "RayRec layout");
-
-__device__ __forceinline__ void ray_load(const RayRec &r, Query &q, int &top) {
-    float4 a = reinterpret_cast<const float4 *>(&r)[0];
-    float4 b = reinterpret_cast<const float4 *>(&r)[1];
-    float4 c = reinterpret_cast<const float4 *>(&r)[2];
-    float4 e = reinterpret_cast<const float4 *>(&r)[3];
-    q.o = {a.x, a.y, a.z};
-    q.d = {a.w, b.x, b.y};
-    q.tmin = b.z;
-    q.tmax = b.w;
-    q.self = __float_as_int(c.x);
-    q.back = __float_as_int(c.y);
-    q.win = __float_as_int(c.z);
-    unsigned fl = __float_as_uint(c.w);
-    q.closest = fl & 1u;
-    q.unb = fl & 2u;
-    q.skipchk = fl & 4u;
-    q.skipped = fl & 8u;
-    q.bf = false;
-    q.mask = {e.x, e.y, e.z};
-    top = __float_as_int(e.w);
-}
-
-__device__ __forceinline__ void ray_store(RayRec &r, const Query &q, int top) {
-    unsigned fl = (q.closest ? 1u : 0u) | (q.unb ? 2u : 0u) | (q.skipchk ? 4u : 0u) | (q.skipped ? 8u : 0u);
-    float4 *w = reinterpret_cast<float4 *>(&r);
-    w[0] = make_float4(q.o.x, q.o.y, q.o.z, q.d.x);
-    w[1] = make_float4(q.d.y, q.d.z, q.tmin, q.tmax);
-    w[2] = make_float4(__int_as_float(q.self), __int_as_float(q.back), __int_as_float(q.win), __uint_as_float(fl));
-    w[3] = make_float4(q.mask.r, q.mask.g, q.mask.b, __int_as_float(top));
-}
-
-// the result fields only (trace -> shade)
-__device__ __forceinline__ void ray_store_result(RayRec &r, const Query &q) {
-    float4 *w = reinterpret_cast<float4 *>(&r);
-    unsigned fl = (q.closest ? 1u : 0u) | (q.unb ? 2u : 0u) | (q.skipchk ? 4u : 0u) | (q.skipped ? 8u : 0u);
-    w[1].w = q.tmax;
-    reinterpret_cast<int *>(&r)[10] = q.win;
-    reinterpret_cast<unsigned *>(&r)[11] = fl;
-    r.mask[0] = q.mask.r;
-    r.mask[1] = q.mask.g;
-    r.mask[2] = q.mask.b;
-}
-
-// wave sum of a counter, one atomic per wave
-__device__ __forceinline__ void wave_add(unsigned long long *dst, unsigned long long v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
-}
-
-__device__ __forceinline__ void flush_counters(const Params &p, const Counters &c) {
-    unsigned long long *st = p.stats;
-    wave_add(&st[0], c.prim);
-    wave_add(&st[1], c.shadow);
-    wave_add(&st[2], c.refr);
-    wave_add(&st[3], c.refl);
-    wave_add(&st[4], c.skip);
-    wave_add(&st[5], c.ub);
-    wave_add(&st[6], c.boxes);
-    wave_add(&st[7], c.ftests);
-    wave_add(&st[8], c.stests);
-}
-
-// primary ray of pixel `idx` (main.cpp:720-729) into path slot `slot`
-__device__ __forceinline__ void spawn_primary(const Params &p, unsigned idx, int slot) {
-    int px, py;
-    pixel_xy(p, idx, px, py);
-    const V3 ul = {p.ul[0], p.ul[1], p.ul[2]}, dh = {p.dh[0], p.dh[1], p.dh[2]}, dv = {p.dv[0], p.dv[1], p.dv[2]};
-    const V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
-    V3 pt = vadd(vadd(ul, vmul(dh, (float)px)), vmul(dv, (float)(py + p.y0)));
-    Query q;
-    q.o = eye;
-    q.d = vnorm(vsub(pt, eye));
-    q.tmin = 0.0f;                     // primary rays accept any t > 0 (main.cpp:736)
-    q.tmax = kFltMax;
-    q.unb = false;
-    q.self = -1;
-    q.back = -1;
-    q.closest = true;
-    q.skipchk = false;
-    q.skipped = false;
-    q.win = -1;
-    q.mask = {1.0f, 1.0f, 1.0f};
-    ray_store(p.rays[slot], q, -1);
-    p.spix[slot] = (int)idx;
-}
-
-// fill every path slot with the first `pool` pixels
-__global__ void __launch_bounds__(kBlock) wf_spawn(Params p) {
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (unsigned base = blockIdx.x * kBlock; base < p.pool; base += gridDim.x * kBlock) {
-        unsigned i = base + threadIdx.x;
-        if (i < p.pool) {
-            spawn_primary(p, i, (int)i);
-            cnt.prim++;
-        }
-    }
-    flush_counters(p, cnt);
-}
-
-template <int MODE>
-__global__ void __launch_bounds__(kBlock) wf_trace(Params p) {
-    extern __shared__ float4 lds[];
-    int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;
-    const unsigned n = *p.cin;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (unsigned base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        unsigned i = base + threadIdx.x;
-        bool act = i < n;
-        int pix = 0;
-        Query q;
-        int top = 0;
-        if (act) {
-            pix = p.qin ? p.qin[i] : (int)i;
-            ray_load(p.rays[pix], q, top);
-        } else {
-            q.tmin = kInf;
-        }
-        if (MODE == MODE_BVH) {
-            q.bf = act && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
-            if (act && !q.bf) bvh_trace(q, p, stk, cnt);
-            bool need = act && q.bf;
-            if (__ballot(need)) scan<false>(q, p, nullptr, nullptr, need, cnt.ftests, cnt.stests);
-        } else {
-            scan<false>(q, p, nullptr, nullptr, act, cnt.ftests, cnt.stests);
-        }
-        if (act) ray_store_result(p.rays[pix], q);
-    }
-    flush_counters(p, cnt);
-}
-
-template <int MAXF>
-__global__ void __launch_bounds__(kBlock) wf_shade(Params p) {
-    const unsigned n = *p.cin;
-    const int lane = threadIdx.x & 63;
-    Counters cnt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    Frame<MAXF> *frames = reinterpret_cast<Frame<MAXF> *>(p.frames);
-    for (unsigned base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        unsigned i = base + threadIdx.x;
-        bool more = false, done = false;
-        int pix = 0;                                 // path slot
-        if (i < n) {
-            pix = p.qin ? p.qin[i] : (int)i;
-            Query q;
-            int top;
-            ray_load(p.rays[pix], q, top);
-            C3 color;
-            more = advance<MAXF>(p, frames + (size_t)pix * MAXF, top, q, cnt, color);
-            if (more) {
-                ray_store(p.rays[pix], q, top);
-            } else {
-                int px, py;
-                pixel_xy(p, (unsigned)p.spix[pix], px, py);
-                float *o = p.out + ((size_t)py * p.W + px) * 3;
-                o[0] = color.r;
-                o[1] = color.g;
-                o[2] = color.b;
-                done = true;
-            }
-        }
-        // refill finished slots with new pixels: ballot + one atomic + mbcnt
-        unsigned long long dm = __ballot(done);
-        if (dm) {
-            int leader = __ffsll((long long)dm) - 1;
-            unsigned b = 0;
-            if (lane == leader) b = atomicAdd(p.work, (unsigned)__popcll(dm));
-            b = __shfl(b, leader);
-            if (done) {
-                unsigned idx = b + (unsigned)__popcll(dm & ((1ull << lane) - 1ull));
-                if (idx < p.total) {
-                    spawn_primary(p, idx, pix);
-                    cnt.prim++;
-                    more = true;
-                }
-            }
-        }
-        // compaction of the follow-up rays: ballot + one atomic + mbcnt
-        unsigned long long m = __ballot(more);
-        if (m) {
-            int leader = __ffsll((long long)m) - 1;
-            unsigned b = 0;
-            if (lane == leader) b = atomicAdd(p.cout, (unsigned)__popcll(m));
-            b = __shfl(b, leader);
-            if (more) p.qout[b + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = pix;
-        }
-    }
-    flush_counters(p, cnt);
+    atomicAdd(&st[6], (unsigned long long)cnt.boxes);
+    atomicAdd(&st[7], (unsigned long long)cnt.ftests);
+    atomicAdd(&st[8], (unsigned long long)cnt.stests);
 }
 
 }  // namespace rt
@@ -1197,9 +951,8 @@ struct rt_scene {
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
-    long long opt_engine = -1;         // -1 auto, 0 megakernel, 1 wavefront
     long long opt_bvh_leaf = 8;        // SAH max leaf size
-    long long opt_bvh_trav = 1000;     // SAH traversal cost, x1000 of a sphere test
+    long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
     struct PrimSrc {
         int key;
@@ -1215,15 +968,6 @@ struct rt_scene {
     int *d_bkeys = nullptr;
     int bvh_depth = 0;
     int bvh_stack = 0;
-    // wavefront engine buffers (grown on demand)
-    RayRec *wf_rays = nullptr;
-    int *wf_spix = nullptr;
-    long long opt_pool = 1 << 20;      // wavefront path slots
-    void *wf_frames = nullptr;
-    int *wf_q[2] = {nullptr, nullptr};
-    unsigned *wf_cnt = nullptr;        // 2 queue lengths
-    size_t wf_cap = 0, wf_frame_bytes = 0;
-    int last_iters = 0;
     bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
     bool last_valid = false;
@@ -1250,7 +994,7 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
-    if (mode == MODE_BVH) return (size_t)std::max(1, s->bvh_stack) * kBlock * sizeof(int);
+    if (mode == MODE_BVH) return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int);
     return 0;
 }
 
@@ -1354,88 +1098,6 @@ int build_bvh(rt_scene *s, double D) {
     return RT_OK;
 }
 
-template <typename K>
-int persistent_grid(K kernel, size_t shm, int num_cu, unsigned work) {
-    int nb = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, shm);
-    long long g = (long long)std::max(1, nb) * num_cu;
-    long long need = ((long long)work + kBlock - 1) / kBlock;
-    return (int)std::max(1LL, std::min(g, need));
-}
-
-int wf_reserve(rt_scene *s, size_t px, size_t frame_bytes) {
-    if (px <= s->wf_cap && frame_bytes * px <= s->wf_frame_bytes) return RT_OK;
-    size_t cap = std::max(px, s->wf_cap);
-    if (s->wf_rays) (void)hipFree(s->wf_rays);
-    if (s->wf_spix) (void)hipFree(s->wf_spix);
-    if (s->wf_frames) (void)hipFree(s->wf_frames);
-    for (int k = 0; k < 2; k++)
-        if (s->wf_q[k]) (void)hipFree(s->wf_q[k]);
-    s->wf_rays = nullptr;
-    s->wf_spix = nullptr;
-    s->wf_frames = nullptr;
-    s->wf_q[0] = s->wf_q[1] = nullptr;
-    s->wf_cap = s->wf_frame_bytes = 0;
-    if (hipMalloc(&s->wf_rays, cap * sizeof(RayRec)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMalloc(&s->wf_spix, cap * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMalloc(&s->wf_frames, cap * frame_bytes) != hipSuccess) return RT_E_NOMEM;
-    for (int k = 0; k < 2; k++)
-        if (hipMalloc(&s->wf_q[k], cap * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
-    if (!s->wf_cnt && hipMalloc(&s->wf_cnt, 4 * sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
-    s->wf_cap = cap;
-    s->wf_frame_bytes = cap * frame_bytes;
-    return RT_OK;
-}
-
-// Wavefront render: spawn, then (trace, shade) until no pixel needs a ray.
-// Iterations run in batches; after each batch the remaining queue length is
-// read back, so the loop ends after (longest pixel's ray count) iterations.
-template <int MAXF>
-int launch_wavefront(rt_scene *s, Params p, int mode, hipStream_t st) {
-    unsigned total = p.total;
-    unsigned pool = (unsigned)std::max(1LL, std::min((long long)total, s->opt_pool));
-    int rc = wf_reserve(s, pool, sizeof(Frame<MAXF>) * MAXF);
-    if (rc) return rc;
-    p.rays = s->wf_rays;
-    p.frames = s->wf_frames;
-    p.spix = s->wf_spix;
-    p.pool = pool;
-    const size_t shm = mode == MODE_BVH ? (size_t)std::max(1, s->bvh_stack) * kBlock * sizeof(int) : 0;
-    // the pool takes pixels [0, pool); refills continue from the work counter
-    if (hipMemsetD32Async((hipDeviceptr_t)s->work, (int)pool, 1, st) != hipSuccess) return RT_E_HIP;
-    int g_spawn = persistent_grid(wf_spawn, 0, s->num_cu, pool);
-    hipLaunchKernelGGL(wf_spawn, dim3(g_spawn), dim3(kBlock), 0, st, p);
-    if (hipMemsetD32Async((hipDeviceptr_t)s->wf_cnt, (int)pool, 1, st) != hipSuccess) return RT_E_HIP;
-    auto trace_k = mode == MODE_BVH ? wf_trace<MODE_BVH> : wf_trace<MODE_SCAN>;
-    int g_trace = persistent_grid(trace_k, shm, s->num_cu, pool);
-    int g_shade = persistent_grid(wf_shade<MAXF>, 0, s->num_cu, pool);
-    // upper bound on iterations: every pixel's TraceRay calls, one per iteration
-    // per slot (primary + (lights + 2) per node), pixels streamed through the pool
-    long long nodes = (1LL << (std::min(p.depth, 20) + 1)) - 1;
-    long long per_px = 1 + (long long)(p.nl + 2) * nodes;
-    long long bound = per_px * (((long long)total + pool - 1) / pool) + per_px;
-    const int batch = 8;
-    int it = 0;
-    unsigned h_left = total;
-    while (it < bound && h_left > 0) {
-        for (int b = 0; b < batch && it < bound; b++, it++) {
-            int cur = it & 1;
-            p.qin = it == 0 ? nullptr : s->wf_q[cur];
-            p.qout = s->wf_q[cur ^ 1];
-            p.cin = s->wf_cnt + cur;
-            p.cout = s->wf_cnt + (cur ^ 1);
-            hipLaunchKernelGGL(trace_k, dim3(g_trace), dim3(kBlock), shm, st, p);
-            if (hipMemsetAsync(s->wf_cnt + (cur ^ 1), 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
-            hipLaunchKernelGGL(wf_shade<MAXF>, dim3(g_shade), dim3(kBlock), 0, st, p);
-        }
-        if (hipMemcpyAsync(&h_left, s->wf_cnt + (it & 1), sizeof(unsigned), hipMemcpyDeviceToHost, st) != hipSuccess)
-            return RT_E_HIP;
-        if (hipStreamSynchronize(st) != hipSuccess) return RT_E_HIP;
-    }
-    s->last_iters = it;
-    return hipGetLastError() == hipSuccess ? RT_OK : RT_E_HIP;
-}
-
 int launch(rt_scene *s, Params &p, hipStream_t st) {
     int depth = p.depth < 0 ? 0 : p.depth;
     if (depth > 16) return RT_E_UNSUPPORTED;
@@ -1458,13 +1120,6 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
         bool lds = s->opt_lds == 1 || (s->opt_lds == -1 && s->lds_bytes <= 64 * 1024);
         if (s->lds_bytes > 64 * 1024) lds = false;
         if (lds) mode = MODE_SCAN_LDS;
-    }
-    bool wavefront = s->opt_engine == 1 || (s->opt_engine == -1 && mode == MODE_BVH);
-    if (wavefront) {
-        int wmode = mode == MODE_BVH ? MODE_BVH : MODE_SCAN;
-        if (depth <= 4) return launch_wavefront<5>(s, p, wmode, st);
-        if (depth <= 8) return launch_wavefront<9>(s, p, wmode, st);
-        return launch_wavefront<17>(s, p, wmode, st);
     }
     hipError_t e;
     if (depth <= 4) e = launch_mode<5>(s, p, mode, st);
@@ -1660,12 +1315,6 @@ int rt_scene_destroy(rt_scene *s) {
     for (void *d : s->allocs) (void)hipFree(d);
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_bkeys) (void)hipFree(s->d_bkeys);
-    if (s->wf_rays) (void)hipFree(s->wf_rays);
-    if (s->wf_spix) (void)hipFree(s->wf_spix);
-    if (s->wf_frames) (void)hipFree(s->wf_frames);
-    for (int k = 0; k < 2; k++)
-        if (s->wf_q[k]) (void)hipFree(s->wf_q[k]);
-    if (s->wf_cnt) (void)hipFree(s->wf_cnt);
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);
@@ -1683,8 +1332,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
-    else if (k == "engine") s->opt_engine = value;
-    else if (k == "pool") s->opt_pool = std::max(64LL, value);
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);

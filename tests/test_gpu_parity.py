@@ -55,21 +55,18 @@ def test_scene_parity(name, golden):
         assert diff_px <= MAX_BAD_FRAC, diff_px
 
 
-@pytest.mark.parametrize("engine", [0, 1])
 @pytest.mark.parametrize("accel", [0, 1])
 @pytest.mark.parametrize("name", golden_names(lambda v: v["width"] * v["height"] <= 300 * 300))
-def test_scene_parity_forced_path(name, accel, engine, golden):
-    """Every search strategy x execution engine on every small fixture: the
-    brute-force scan (accel=0) and the BVH (accel=1, with its exact
-    fallbacks), run by the persistent megakernel (engine=0) or the wavefront
-    trace/shade kernels (engine=1), each against the oracle, with identical
-    ray counts."""
-    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel, "engine": engine})
+def test_scene_parity_forced_path(name, accel, golden):
+    """Both search strategies on every small fixture: the brute-force scan
+    (accel=0) and the BVH (accel=1, with its exact fallbacks), each against
+    the oracle, with identical ray counts."""
+    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel})
     ref, cnt = OracleScene(name, cwd=SCENES).render()
     c = compare(img, ref)
-    _summary[f"{name}@accel{accel}e{engine}"] = dict(c, tests=dict(box=st.box_tests, face=st.face_tests,
-                                                                   sphere=st.sphere_tests))
-    assert_parity(img, ref, f"{name} accel={accel} engine={engine}")
+    _summary[f"{name}@accel{accel}"] = dict(c, tests=dict(box=st.box_tests, face=st.face_tests,
+                                                          sphere=st.sphere_tests))
+    assert_parity(img, ref, f"{name} accel={accel}")
     assert _counts(st) == cnt
 
 
