@@ -9,10 +9,10 @@ SURVEY.md §8a).  Workload (N=1 and the default): config C3 of BASELINE.json,
 4096x4096, 1000 spheres + 1000 triangles, reflection/refraction depth 4,
 seeded synthetic scene (simple-raytracer_amd/rtamd/scenes.py).
 
-Multi-GPU (torchrun, one process per GPU): the image's rows are split into
-contiguous strips, one per rank (strong scaling: the image is fixed); each
-rank renders its strip into HBM and the strips are gathered to rank 0 over
-RCCL (torch.distributed "nccl").  Timed region: barrier + synchronize on both
+Multi-GPU (torchrun, one process per GPU): the image's rows are dealt to the
+ranks in 8-row blocks, round robin (strong scaling: the image is fixed); each
+rank renders its rows into HBM and the row sets are gathered to rank 0 over
+RCCL (torch.distributed "nccl") and put back in image order.  Timed region: barrier + synchronize on both
 sides, K steps, max over ranks.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -134,9 +134,10 @@ def main() -> None:
         k, v = kv.split("=")
         gs.set_option(k, int(v))
 
-    # strong scaling: contiguous row strips, equal counts for the gather
-    from rtamd.dist import alloc_strips, gather_strips, strip_rows
-    y0, y1, _ = strip_rows(H, world, rank)
+    # strong scaling: block-interleaved row sets (rtamd/dist.py), equal-size
+    # buffers for the gather
+    from rtamd.dist import alloc_strips, gather_strips, row_set
+    ry0, rblock, rstep, nrows, _ = row_set(H, world, rank)
     strip, gather_list = alloc_strips(H, W, world, rank, "cuda", torch)
     # a dedicated (non-null) stream: the render kernel, its timing events and
     # the RCCL gather are all ordered on it
@@ -145,8 +146,9 @@ def main() -> None:
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        if y1 > y0:
-            gs.render_rows_async(cam, W, H, y0, y1, strip.data_ptr(), stream.cuda_stream)
+        if nrows > 0:
+            gs.render_row_blocks_async(cam, W, H, ry0, rblock, rstep, nrows, strip.data_ptr(),
+                                       stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
@@ -194,7 +196,7 @@ def main() -> None:
         flops = st.box_tests * FLOP_BOX + st.face_tests * FLOP_TRI + st.sphere_tests * FLOP_SPHERE
         achieved = flops / k_s / 1e12
         bf_equiv = my_rays * bf_flop_per_ray / k_s / 1e12
-        px = (y1 - y0) * W
+        px = nrows * W
         scene_bytes = 80 * nt + 16 * ns + 52 * (ns + nt)
         alg_bytes = 12 * px + scene_bytes
         traffic = load_pmc_traffic(args.config)
@@ -222,7 +224,7 @@ def main() -> None:
             "data": "synthetic (seeded scene generator, rtamd/scenes.py)",
             "config": {"workload": WORKLOADS[args.config], "imsize": [W, H], "spheres": ns,
                        "triangles": nt, "depth": cfg["depth"], "lights": 2,
-                       "rays_per_step": int(rays_total), "parallelism": f"row-strips x{world}"
+                       "rays_per_step": int(rays_total), "parallelism": f"interleaved 8-row blocks x{world}"
                        + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),

@@ -149,6 +149,13 @@ int rt_render_rows_async(rt_scene *scene, const rt_camera *cam, int W, int H, in
                          void *hip_stream);
 int rt_scene_last_stats(rt_scene *scene, rt_stats *stats);
 
+/* Block-interleaved row set, asynchronous (device out_rgb): local row r
+ * (0 <= r < nrows) is image row y0 + (r / block) * step + r % block, written
+ * to out_rgb row r.  With y0 = 8*rank, block = 8, step = 8*N the N ranks of a
+ * multi-GPU render get equally mixed rows (load balance). */
+int rt_render_row_blocks_async(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,
+                               int nrows, float *out_rgb, void *hip_stream);
+
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
  * (persistent blocks, 0 = occupancy), "depth" (recursion depth override). */

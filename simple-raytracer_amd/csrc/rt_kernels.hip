@@ -139,7 +139,8 @@ struct Params {
     float eta_bkg, eps;
     int depth;
     float eye[3], ul[3], dh[3], dv[3];
-    int W, y0, rows;                     // render rows [y0, y0 + rows) of a W-wide image
+    int W, y0, rows;                     // render `rows` rows of a W-wide image: local row r is
+    int rblock, rstep;                   // image row y0 + (r / rblock) * rstep + r % rblock
     unsigned int total;                  // W * rows
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
@@ -817,6 +818,11 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
 
 // Pixel index -> (x, y): strips of 8 rows, 8x8 blocks along the strip, so a
 // wave's 64 consecutive indices cover an 8x8 tile.
+// image row of local row r (block-interleaved row sets for multi-GPU balance)
+__device__ __forceinline__ int image_row(const Params &p, int r) {
+    return p.y0 + (r / p.rblock) * p.rstep + r % p.rblock;
+}
+
 __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, int &y) {
     unsigned strip_px = (unsigned)p.W * 8u;
     unsigned s = idx / strip_px;
@@ -880,7 +886,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     if (idx < p.total) {
                         pixel_xy(p, idx, px, py);
                         V3 pt = vadd(vadd(V3{p.ul[0], p.ul[1], p.ul[2]}, vmul(V3{p.dh[0], p.dh[1], p.dh[2]}, (float)px)),
-                                     vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)(py + p.y0)));
+                                     vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)image_row(p, py)));
                         V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
                         q.o = eye;
                         q.d = vnorm(vsub(pt, eye));
@@ -1341,10 +1347,13 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     return RT_OK;
 }
 
-int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
-                         void *hip_stream) {
-    if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || y1 > H || y0 >= y1) return RT_E_INVALID;
-    if ((long long)W * (y1 - y0) >= (1ll << 31)) return RT_E_UNSUPPORTED;
+int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int block, int step,
+                               int nrows, float *out_rgb, void *hip_stream) {
+    if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || block < 1 || step < block || nrows < 1)
+        return RT_E_INVALID;
+    long long last = (long long)y0 + (long long)((nrows - 1) / block) * step + (nrows - 1) % block;
+    if (last >= H) return RT_E_INVALID;
+    if ((long long)W * nrows >= (1ll << 31)) return RT_E_UNSUPPORTED;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : s->stream;
     Params p = s->base;
@@ -1356,8 +1365,10 @@ int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0
     }
     p.W = W;
     p.y0 = y0;
-    p.rows = y1 - y0;
-    p.total = (unsigned)((long long)W * (y1 - y0));
+    p.rows = nrows;
+    p.rblock = block;
+    p.rstep = step;
+    p.total = (unsigned)((long long)W * nrows);
     p.out = out_rgb;
     if (hipMemsetAsync(s->work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
     if (hipMemsetAsync(s->stats, 0, 16 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
@@ -1367,6 +1378,12 @@ int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0
     s->last_stream = st;
     s->last_valid = rc == RT_OK;
     return rc;
+}
+
+int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
+                         void *hip_stream) {
+    if (y1 <= y0) return RT_E_INVALID;
+    return rt_render_row_blocks_async(s, cam, W, H, y0, y1 - y0, y1 - y0, y1 - y0, out_rgb, hip_stream);
 }
 
 int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {

@@ -86,7 +86,8 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
                 "rth_output_path"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
-               "rt_render_rows_async", "rt_scene_last_stats", "rt_scene_set_option", "rt_strerror"]
+               "rt_render_rows_async", "rt_render_row_blocks_async", "rt_scene_last_stats",
+               "rt_scene_set_option", "rt_strerror"]
 
 
 def host_lib() -> C.CDLL:
@@ -135,6 +136,9 @@ def hip_lib() -> C.CDLL:
                                      C.c_int, C.c_void_p, C.POINTER(rt_stats)]
         L.rt_render_rows_async.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int,
                                            C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.rt_render_row_blocks_async.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int,
+                                                 C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                                 C.c_void_p]
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
@@ -186,7 +190,10 @@ class HostScene:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            host_lib().rth_free(self._h)
+            try:
+                host_lib().rth_free(self._h)
+            except Exception:        # interpreter shutdown
+                pass
             self._h = None
 
     __del__ = close
@@ -253,7 +260,10 @@ class GpuScene:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            hip_lib().rt_scene_destroy(self._h)
+            try:
+                hip_lib().rt_scene_destroy(self._h)
+            except Exception:        # interpreter shutdown
+                pass
             self._h = None
 
     __del__ = close
@@ -277,6 +287,12 @@ class GpuScene:
         _check(hip_lib().rt_render_rows_async(self._h, C.byref(cam), W, H, y0, y1,
                                               C.c_void_p(dev_ptr), C.c_void_p(stream or 0)),
                "rt_render_rows_async")
+
+    def render_row_blocks_async(self, cam: rt_camera, W: int, H: int, y0: int, block: int, step: int,
+                                nrows: int, dev_ptr: int, stream: int | None = None) -> None:
+        _check(hip_lib().rt_render_row_blocks_async(self._h, C.byref(cam), W, H, y0, block, step, nrows,
+                                                    C.c_void_p(dev_ptr), C.c_void_p(stream or 0)),
+               "rt_render_row_blocks_async")
 
     def last_stats(self) -> rt_stats:
         st = rt_stats()

@@ -1,25 +1,36 @@
-"""Row-strip sharding of one image across ranks (one process per GPU).
+"""Row sharding of one image across ranks (one process per GPU).
 
-Every pixel is independent, so the image's rows are cut into
-one contiguous strip per rank, padded to equal height so the strips can be
-gathered with one fixed-count collective.  Each rank renders its strip into
-HBM; rank 0 receives all strips (RCCL over xGMI when the backend is "nccl",
-gloo on CPU in tests) and drops the padding rows.
+Every pixel is independent.  Rows are dealt to ranks in
+blocks of BLOCK rows, round robin (rank r gets row blocks r, r+N, r+2N, ...),
+so every rank gets the same mix of cheap sky rows and expensive glass rows
+(contiguous strips measured 82 % balanced at N = 8 on C3).  Each rank renders
+its rows into an HBM buffer padded to the largest rank's row count; rank 0
+gathers the N buffers with one fixed-count collective (RCCL over xGMI with the
+"nccl" backend, gloo on CPU in tests) and scatters rows back to image order.
 """
 from __future__ import annotations
 
+BLOCK = 8
 
-def strip_rows(H: int, world: int, rank: int) -> tuple[int, int, int]:
-    """(y0, y1, rows_per): rank's rows [y0, y1) and the padded strip height."""
-    rows_per = (H + world - 1) // world
-    y0 = min(H, rank * rows_per)
-    y1 = min(H, y0 + rows_per)
-    return y0, y1, rows_per
+
+def row_set(H: int, world: int, rank: int, block: int = BLOCK) -> tuple[int, int, int, int, int]:
+    """(y0, block, step, nrows, rows_per) for rt_render_row_blocks_async:
+    local row k is image row y0 + (k // block) * step + k % block."""
+    nblocks = (H + block - 1) // block
+    mine = list(range(rank, nblocks, world))
+    nrows = sum(min(block, H - b * block) for b in mine)
+    rows_per = max(sum(min(block, H - b * block) for b in range(r, nblocks, world)) for r in range(world))
+    return rank * block, block, block * world, nrows, max(rows_per, 1)
+
+
+def image_rows(H: int, world: int, rank: int, block: int = BLOCK) -> list[int]:
+    y0, b, step, nrows, _ = row_set(H, world, rank, block)
+    return [y0 + (k // b) * step + k % b for k in range(nrows)]
 
 
 def alloc_strips(H: int, W: int, world: int, rank: int, device, torch):
-    """This rank's padded strip buffer and, on rank 0, the gather targets."""
-    _, _, rows_per = strip_rows(H, world, rank)
+    """This rank's padded row buffer and, on rank 0, the gather targets."""
+    *_, rows_per = row_set(H, world, rank)
     strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device=device)
     targets = None
     if world > 1 and rank == 0:
@@ -28,11 +39,17 @@ def alloc_strips(H: int, W: int, world: int, rank: int, device, torch):
 
 
 def gather_strips(strip, targets, world: int, rank: int, H: int, dist, torch):
-    """Collect every rank's strip on rank 0; returns the H x W x 3 image there
-    (None elsewhere).  One gather of world equal-size strips."""
+    """Collect every rank's rows on rank 0 and put them in image order;
+    returns the H x W x 3 image there (None elsewhere)."""
     if world == 1:
         return strip[:H]
     dist.gather(strip, targets, dst=0)
     if rank != 0:
         return None
-    return torch.cat(targets, dim=0)[:H]
+    img = torch.empty((H,) + tuple(strip.shape[1:]), dtype=strip.dtype, device=strip.device)
+    for r in range(world):
+        rows = image_rows(H, world, r)
+        if rows:
+            idx = torch.tensor(rows, dtype=torch.long, device=strip.device)
+            img.index_copy_(0, idx, targets[r][: len(rows)])
+    return img

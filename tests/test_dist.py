@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import SCENES
-from rtamd.dist import alloc_strips, gather_strips, strip_rows
+from rtamd.dist import alloc_strips, gather_strips, image_rows, row_set
 
 
 def _free_port() -> int:
@@ -30,11 +30,11 @@ def _worker(rank, world, port, scene, out_q):
     from oracle_py import OracleScene
     sc = OracleScene(scene, cwd=SCENES)
     W, H = sc.width, sc.height
-    y0, y1, rows_per = strip_rows(H, world, rank)
+    rows = image_rows(H, world, rank)
     strip, targets = alloc_strips(H, W, world, rank, "cpu", torch)
-    if y1 > y0:
-        img, _ = sc.render(rows=np.arange(y0, y1))
-        strip[: y1 - y0] = torch.from_numpy(img)
+    if rows:
+        img, _ = sc.render(rows=np.array(rows))
+        strip[: len(rows)] = torch.from_numpy(img)
     full = gather_strips(strip, targets, world, rank, H, dist, torch)
     if rank == 0:
         out_q.put(full.numpy())
@@ -42,7 +42,7 @@ def _worker(rank, world, port, scene, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 5])
 def test_gather_reassembles_image(world):
     scene = "test7_s.txt"
     ctx = mp.get_context("spawn")
@@ -60,12 +60,14 @@ def test_gather_reassembles_image(world):
     assert np.array_equal(np.nan_to_num(full, nan=-9), np.nan_to_num(ref, nan=-9))
 
 
-def test_strip_rows_cover_image():
-    for H in (1, 7, 64, 4096, 4097):
+def test_row_sets_cover_image():
+    for H in (1, 7, 64, 100, 4096, 4097):
         for world in (1, 2, 3, 8):
             rows = []
             for r in range(world):
-                y0, y1, per = strip_rows(H, world, r)
-                assert 0 <= y1 - y0 <= per
-                rows += list(range(y0, y1))
-            assert rows == list(range(H))
+                y0, b, step, n, per = row_set(H, world, r)
+                assert 0 <= n <= per
+                rr = image_rows(H, world, r)
+                assert len(rr) == n and all(0 <= y < H for y in rr)
+                rows += rr
+            assert sorted(rows) == list(range(H))
