@@ -1157,7 +1157,8 @@ int launch_ordering(rt_scene *s, Params &p, int mode, hipStream_t st) {
     if (hipMemsetAsync(s->d_classes, 0, 8 * sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
     p.phit = s->d_phit;
     p.classes = s->d_classes;
-    p.order = nullptr;
+    p.order = s->d_order;              // written by order_pass, read by the render kernel
+    if (!p.phit || !p.order || !p.classes || s->order_cap < p.total) return RT_E_INVALID;
     size_t shm = mode_lds_bytes(s, MODE_BVH);
     auto pk = mode == MODE_BVH ? primary_pass<MODE_BVH> : primary_pass<MODE_SCAN>;
     if (mode != MODE_BVH) shm = 0;
@@ -1169,7 +1170,6 @@ int launch_ordering(rt_scene *s, Params &p, int mode, hipStream_t st) {
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, order_pass, kBlock, 0);
     g = (int)std::max(1LL, std::min((long long)std::max(1, nb) * s->num_cu, need));
     hipLaunchKernelGGL(order_pass, dim3(g), dim3(kBlock), 0, st, p);
-    p.order = s->d_order;
     return hipGetLastError() == hipSuccess ? RT_OK : RT_E_HIP;
 }
 

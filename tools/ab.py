@@ -43,10 +43,9 @@ def main():
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
             line = next((l for l in p.stdout.splitlines() if l.startswith("{")), None)
             if p.returncode != 0 or line is None:
+                # any failure may be a GPU fault: stop using the GPU in this call
                 print(f"{name}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
-                if p.returncode < 0 or p.returncode in (124, 134, 137, 139):
-                    sys.exit(1)          # a crash: stop using the GPU
-                continue
+                sys.exit(1)
             j = json.loads(line)
             j["ab_name"], j["ab_round"] = name, r
             out.write(json.dumps(j) + "\n")
