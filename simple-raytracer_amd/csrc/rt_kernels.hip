@@ -145,11 +145,6 @@ struct Params {
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
     const int *__restrict__ bkeys;
-    // cost-ordered scheduling (order != NULL): primary hits traced by
-    // primary_pass, pixels issued most-expensive class first
-    int2 *__restrict__ phit;             // [total] (winning object, t bits) of the primary ray
-    unsigned *__restrict__ order;        // [total] pixel indices in issue order
-    unsigned *__restrict__ classes;      // [8] per-class counts, per-class cursors
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
 };
@@ -858,12 +853,23 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     int *stk = hits + kHits * kBlock;                       //           stack[k * kBlock]
     Query q;
     bool busy = false;         // lane owns a pixel
-    bool need_scan = false;    // q holds a TraceRay to run
-    bool has_result = false;   // q holds a TraceRay result to consume
+    bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
     int px = 0, py = 0;
     for (;;) {
         int kind = RK_NONE;
+        if (pending) {
+            C3 color;
+            kind = advance<MAXF>(p, ls, q, cnt, color);
+            pending = kind != RK_NONE;
+            if (!pending) {
+                float *o = p.out + ((size_t)py * p.W + px) * 3;
+                o[0] = color.r;
+                o[1] = color.g;
+                o[2] = color.b;
+                busy = false;
+            }
+        }
         // refill idle lanes: ballot + one atomic per wave + mbcnt prefix
         if (!drained) {
             unsigned long long idle = __ballot(!busy);
@@ -876,9 +882,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 if (base + n >= p.total) drained = true;
                 if (!busy) {
                     unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
-                    unsigned slot = base + rank;
-                    if (slot < p.total) {
-                        unsigned idx = p.order ? p.order[slot] : slot;
+                    unsigned idx = base + rank;
+                    if (idx < p.total) {
                         pixel_xy(p, idx, px, py);
                         V3 pt = vadd(vadd(V3{p.ul[0], p.ul[1], p.ul[2]}, vmul(V3{p.dh[0], p.dh[1], p.dh[2]}, (float)px)),
                                      vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)image_row(p, py)));
@@ -894,52 +899,27 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                         q.skipped = false;
                         q.win = -1;
                         ls.top = -1;
+                        kind = RK_PRIMARY;
                         busy = true;
-                        if (p.order) {               // already traced by primary_pass
-                            int2 h = p.phit[idx];
-                            q.win = h.x;
-                            if (h.x >= 0) q.tmax = __int_as_float(h.y);
-                            has_result = true;
-                        } else {
-                            kind = RK_PRIMARY;
-                            need_scan = true;
-                        }
+                        pending = true;
                     }
                 }
             }
         }
-        if (has_result) {
-            C3 color;
-            kind = advance<MAXF>(p, ls, q, cnt, color);
-            has_result = false;
-            need_scan = kind != RK_NONE;
-            if (!need_scan) {
-                float *o = p.out + ((size_t)py * p.W + px) * 3;
-                o[0] = color.r;
-                o[1] = color.g;
-                o[2] = color.b;
-                busy = false;
-            }
-        }
+        if (!pending) q.tmin = kInf;                 // lane sits this scan out
+        if (__ballot(pending) == 0ull) break;
         w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
         w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
         w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
-        if (__ballot(need_scan) == 0ull) {
-            if (drained) break;
-            continue;                                // every lane idle: refill
-        }
-        if (!need_scan) q.tmin = kInf;               // lane sits this scan out
         if (MODE == MODE_BVH) {
-            q.bf = need_scan && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
-            if (need_scan && !q.bf) bvh_trace(q, p, stk, hits, cnt);
-            bool need = need_scan && q.bf;
+            q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
+            bool need = pending && q.bf;
             if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
         } else {
-            scan<SRC_LDS>(q, p, lds_f, lds_s, need_scan, cnt.ftests, cnt.stests);
+            scan<SRC_LDS>(q, p, lds_f, lds_s, pending, cnt.ftests, cnt.stests);
         }
-        has_result = need_scan;
-        need_scan = false;
     }
     unsigned long long *st = p.stats;
     if (lane == 0) {
@@ -953,105 +933,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&st[6], (unsigned long long)cnt.boxes);
     atomicAdd(&st[7], (unsigned long long)cnt.ftests);
     atomicAdd(&st[8], (unsigned long long)cnt.stests);
-}
-
-
-// ---------------------------------------------------------------------------
-// Cost-ordered scheduling.  primary_pass traces every pixel's primary ray
-// (main.cpp:720-742; a coherent, lean launch) and classifies the pixel by what
-// it hit: 3 transparent (refraction recursion), 2 reflective (ks > 0),
-// 1 other surface, 0 miss.  order_pass lists the pixels by class, most
-// expensive first, so the deep glass paths start early instead of forming the
-// launch's tail, and similar pixels share waves.  The render kernel then takes
-// pixels from that order and consumes the stored primary hit.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int pixel_class(const Params &p, int win) {
-    if (win < 0) return 0;
-    const ObjK &ob = p.objs[win];
-    if ((double)ob.opacity < 1.0 && ob.eta > 0) return 3;
-    if (ob.ks > 0.0f) return 2;
-    return 1;
-}
-
-template <int MODE>
-__global__ void __launch_bounds__(kBlock) primary_pass(Params p) {
-    extern __shared__ float4 lds[];
-    int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;
-    int *stk = hits + kHits * kBlock;
-    const int lane = threadIdx.x & 63;
-    Counters cnt = {0, 0, 0, 0, 0};
-    unsigned long long w_prim = 0;
-    unsigned wc[4] = {0, 0, 0, 0};
-    const V3 ul = {p.ul[0], p.ul[1], p.ul[2]}, dh = {p.dh[0], p.dh[1], p.dh[2]}, dv = {p.dv[0], p.dv[1], p.dv[2]};
-    const V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
-    for (unsigned base = blockIdx.x * kBlock; base < p.total; base += gridDim.x * kBlock) {
-        unsigned idx = base + threadIdx.x;
-        bool act = idx < p.total;
-        Query q;
-        q.tmin = kInf;
-        if (act) {
-            int px, py;
-            pixel_xy(p, idx, px, py);
-            V3 pt = vadd(vadd(ul, vmul(dh, (float)px)), vmul(dv, (float)image_row(p, py)));
-            q.o = eye;
-            q.d = vnorm(vsub(pt, eye));
-            q.tmin = 0.0f;
-            q.tmax = kFltMax;
-            q.unb = false;
-            q.self = -1;
-            q.back = -1;
-            q.closest = true;
-            q.skipchk = false;
-            q.skipped = false;
-            q.bf = false;
-            q.win = -1;
-            q.mask = {1.0f, 1.0f, 1.0f};
-        }
-        if (MODE == MODE_BVH) {
-            if (act) bvh_trace(q, p, stk, hits, cnt);
-        } else {
-            scan<false>(q, p, nullptr, nullptr, act, cnt.ftests, cnt.stests);
-        }
-        int c = 0;
-        if (act) {
-            p.phit[idx] = make_int2(q.win, __float_as_int(q.tmax));
-            c = pixel_class(p, q.win);
-        }
-        w_prim += (unsigned long long)__popcll(__ballot(act));
-#pragma unroll
-        for (int k = 0; k < 4; k++) wc[k] += (unsigned)__popcll(__ballot(act && c == k));
-    }
-    if (lane == 0) {
-        atomicAdd(&p.stats[0], w_prim);
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (wc[k]) atomicAdd(&p.classes[k], wc[k]);
-    }
-    atomicAdd(&p.stats[6], (unsigned long long)cnt.boxes);
-    atomicAdd(&p.stats[7], (unsigned long long)cnt.ftests);
-    atomicAdd(&p.stats[8], (unsigned long long)cnt.stests);
-}
-
-__global__ void __launch_bounds__(kBlock) order_pass(Params p) {
-    const int lane = threadIdx.x & 63;
-    const unsigned n3 = p.classes[3], n2 = p.classes[2], n1 = p.classes[1];
-    const unsigned off[4] = {n3 + n2 + n1, n3 + n2, n3, 0};
-    for (unsigned base = blockIdx.x * kBlock; base < p.total; base += gridDim.x * kBlock) {
-        unsigned idx = base + threadIdx.x;
-        bool act = idx < p.total;
-        int c = act ? pixel_class(p, p.phit[idx].x) : -1;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            unsigned long long m = __ballot(c == k);
-            if (m) {
-                int leader = __ffsll((long long)m) - 1;
-                unsigned b = 0;
-                if (lane == leader) b = atomicAdd(&p.classes[4 + k], (unsigned)__popcll(m));
-                b = __shfl(b, leader);
-                if (c == k) p.order[off[k] + b + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = idx;
-            }
-        }
-    }
 }
 
 }  // namespace rt
@@ -1076,10 +957,6 @@ struct rt_scene {
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
-    long long opt_order = -1;          // -1 auto (BVH), 0 off, 1 cost-ordered scheduling
-    int2 *d_phit = nullptr;
-    unsigned *d_order = nullptr, *d_classes = nullptr;
-    size_t order_cap = 0;
     long long opt_bvh_leaf = 8;        // SAH max leaf size
     long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
@@ -1139,38 +1016,6 @@ hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, p);
     return hipGetLastError();
-}
-
-// primary_pass + order_pass into the scene's scheduling buffers (p.order set).
-int launch_ordering(rt_scene *s, Params &p, int mode, hipStream_t st) {
-    if (s->order_cap < p.total) {
-        if (s->d_phit) (void)hipFree(s->d_phit);
-        if (s->d_order) (void)hipFree(s->d_order);
-        s->d_phit = nullptr;
-        s->d_order = nullptr;
-        s->order_cap = 0;
-        if (hipMalloc(&s->d_phit, (size_t)p.total * sizeof(int2)) != hipSuccess) return RT_E_NOMEM;
-        if (hipMalloc(&s->d_order, (size_t)p.total * sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
-        s->order_cap = p.total;
-    }
-    if (!s->d_classes && hipMalloc(&s->d_classes, 8 * sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMemsetAsync(s->d_classes, 0, 8 * sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
-    p.phit = s->d_phit;
-    p.classes = s->d_classes;
-    p.order = s->d_order;              // written by order_pass, read by the render kernel
-    if (!p.phit || !p.order || !p.classes || s->order_cap < p.total) return RT_E_INVALID;
-    size_t shm = mode_lds_bytes(s, MODE_BVH);
-    auto pk = mode == MODE_BVH ? primary_pass<MODE_BVH> : primary_pass<MODE_SCAN>;
-    if (mode != MODE_BVH) shm = 0;
-    int nb = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pk, kBlock, shm);
-    long long need = ((long long)p.total + kBlock - 1) / kBlock;
-    int g = (int)std::max(1LL, std::min((long long)std::max(1, nb) * s->num_cu, need));
-    hipLaunchKernelGGL(pk, dim3(g), dim3(kBlock), shm, st, p);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, order_pass, kBlock, 0);
-    g = (int)std::max(1LL, std::min((long long)std::max(1, nb) * s->num_cu, need));
-    hipLaunchKernelGGL(order_pass, dim3(g), dim3(kBlock), 0, st, p);
-    return hipGetLastError() == hipSuccess ? RT_OK : RT_E_HIP;
 }
 
 template <int MAXF>
@@ -1281,12 +1126,6 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
         bool lds = s->opt_lds == 1 || (s->opt_lds == -1 && s->lds_bytes <= 64 * 1024);
         if (s->lds_bytes > 64 * 1024) lds = false;
         if (lds) mode = MODE_SCAN_LDS;
-    }
-    p.order = nullptr;
-    bool ordered = s->opt_order == 1 || (s->opt_order == -1 && mode == MODE_BVH);
-    if (ordered) {
-        int rc = launch_ordering(s, p, mode == MODE_BVH ? MODE_BVH : MODE_SCAN, st);
-        if (rc) return rc;
     }
     hipError_t e;
     if (depth <= 4) e = launch_mode<5>(s, p, mode, st);
@@ -1482,9 +1321,6 @@ int rt_scene_destroy(rt_scene *s) {
     for (void *d : s->allocs) (void)hipFree(d);
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_bkeys) (void)hipFree(s->d_bkeys);
-    if (s->d_phit) (void)hipFree(s->d_phit);
-    if (s->d_order) (void)hipFree(s->d_order);
-    if (s->d_classes) (void)hipFree(s->d_classes);
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);
@@ -1502,7 +1338,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
-    else if (k == "order") s->opt_order = value;
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);
