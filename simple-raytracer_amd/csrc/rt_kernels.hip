@@ -147,6 +147,8 @@ struct Params {
     const int *__restrict__ bkeys;
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
+    int susp_lanes;                      // BVH: suspend a trace when fewer lanes than this still traverse
+    int susp_iter;                       //      ... and the lane made at least this many steps (0 = never)
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -172,6 +174,7 @@ struct Query {
     bool closest, unb, skipchk, skipped;
     bool bf;                              // BVH mode: this query needs the brute-force scan
     C3 mask;
+    int trav;                             // BVH mode: 0 fresh, else suspended trace (sp | nh << 8)
 };
 
 constexpr float kInf = __builtin_huge_valf();
@@ -302,16 +305,26 @@ __device__ __forceinline__ void slab(float lx, float ly, float lz, float hx, flo
 
 // stk: this lane's stack (entries kBlock apart); hits: its kHits-entry list of
 // shadow-hit object keys (also kBlock apart), both in LDS.
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
+//
+// Dynamic fetch (Aila & Laine 2009): once fewer than p.susp_lanes lanes of the
+// wave are still traversing, a lane that has made p.susp_iter steps suspends
+// at its next pop -- the node stays on its LDS stack, (sp, nh) go to q.trav,
+// the running closest hit to q.tmax / q.win -- so that the finished lanes can
+// shade and fetch new rays instead of idling behind the long ones.  The
+// result does not depend on where a trace is cut.  Returns true if suspended.
+__device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
     const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
-    int win = -1;
-    int nh = 0;
+    int win = q.win;                           // -1 on a fresh closest query
+    int nh = q.trav >> 8;
     bool opaque = false;
-    int sp = 0;
+    int sp = q.trav & 255;
     int node = 0;
+    if (sp) node = stk[(--sp) * kBlock];
+    q.trav = 0;
+    int steps = 0;
     for (;;) {
         if (node >= 0) {
             // 4-wide node: lo.x/y/z rows, hi.x/y/z rows, links (rt_bvh.h Node4)
@@ -396,6 +409,15 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             if (opaque || q.bf) break;
         }
         if (sp == 0) break;
+        if (++steps >= p.susp_iter && p.susp_iter > 0 &&
+            __popcll(__builtin_amdgcn_read_exec()) < (unsigned)p.susp_lanes) {
+            q.trav = sp | (nh << 8);
+            if (q.closest) {
+                q.tmax = best;
+                q.win = win;
+            }
+            return true;
+        }
         sp--;
         node = stk[sp * kBlock];
     }
@@ -421,6 +443,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             for (int i = 0; i < nh; i++) q.mask = cmulf(q.mask, cst(p.ofac)[hits[i * kBlock]]);
         }
     }
+    return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -855,10 +878,12 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
+    bool suspended = false;    // MODE_BVH: q's trace was cut short, resume it
     int px = 0, py = 0;
+    q.trav = 0;
     for (;;) {
         int kind = RK_NONE;
-        if (pending) {
+        if (pending && !suspended) {
             C3 color;
             kind = advance<MAXF>(p, ls, q, cnt, color);
             pending = kind != RK_NONE;
@@ -914,7 +939,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         if (MODE == MODE_BVH) {
             q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
-            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
+            if (pending && !q.bf) suspended = bvh_trace(q, p, stk, hits, cnt);
             bool need = pending && q.bf;
             if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
         } else {
@@ -1338,6 +1363,8 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
+    else if (k == "susp") s->base.susp_lanes = (int)std::max(0LL, std::min(64LL, value));
+    else if (k == "susp_iter") s->base.susp_iter = (int)std::max(0LL, value);
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);
