@@ -152,6 +152,9 @@ struct Params {
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
+#ifndef RT_PROF
+#define RT_PROF 0                        // 1: per-wave cycle/occupancy counters in stats[9..15]
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif
@@ -285,6 +288,9 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 struct Counters {
     unsigned skip, ub;
     unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
+#if RT_PROF
+    unsigned trips;                             // traversal loop iterations of this lane
+#endif
 };
 enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
@@ -326,6 +332,9 @@ __device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     q.trav = 0;
     int steps = 0;
     for (;;) {
+#if RT_PROF
+        cnt.trips++;
+#endif
         if (node >= 0) {
             // 4-wide node: lo.x/y/z rows, hi.x/y/z rows, links (rt_bvh.h Node4)
             const float4 *N = p.bvh + 8 * node;
@@ -881,7 +890,14 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool suspended = false;    // MODE_BVH: q's trace was cut short, resume it
     int px = 0, py = 0;
     q.trav = 0;
+#if RT_PROF
+    cnt.trips = 0;
+    unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
+#endif
     for (;;) {
+#if RT_PROF
+        unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
         int kind = RK_NONE;
         if (pending && !suspended) {
             C3 color;
@@ -939,9 +955,26 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         if (MODE == MODE_BVH) {
             q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+#if RT_PROF
+            unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            pc_shade += c1 - c0;
+            pc_iter++;
+            pc_lanes += (unsigned long long)__popcll(__ballot(pending && !q.bf));
+            unsigned tr0 = cnt.trips;
+#endif
             if (pending && !q.bf) suspended = bvh_trace(q, p, stk, hits, cnt);
+#if RT_PROF
+            int d = (int)(cnt.trips - tr0);
+            for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
+            pc_wtrips += (unsigned long long)d;
+            unsigned long long c2 = __builtin_amdgcn_s_memtime();
+            pc_trace += c2 - c1;
+#endif
             bool need = pending && q.bf;
             if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
+#if RT_PROF
+            pc_bf += __builtin_amdgcn_s_memtime() - c2;
+#endif
         } else {
             scan<SRC_LDS>(q, p, lds_f, lds_s, pending, cnt.ftests, cnt.stests);
         }
@@ -958,6 +991,17 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&st[6], (unsigned long long)cnt.boxes);
     atomicAdd(&st[7], (unsigned long long)cnt.ftests);
     atomicAdd(&st[8], (unsigned long long)cnt.stests);
+#if RT_PROF
+    if (lane == 0) {
+        atomicAdd(&st[9], pc_shade);
+        atomicAdd(&st[10], pc_trace);
+        atomicAdd(&st[11], pc_bf);
+        atomicAdd(&st[12], pc_iter);
+        atomicAdd(&st[13], pc_lanes);
+        atomicAdd(&st[14], pc_wtrips);
+    }
+    atomicAdd(&st[15], (unsigned long long)cnt.trips);
+#endif
 }
 
 }  // namespace rt
@@ -1432,6 +1476,16 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, s->ev0, s->ev1);
     stats->kernel_ms = ms;
+    return RT_OK;
+}
+
+int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
+    if (!s || !out || n < 0 || n > 16 || !s->last_valid) return RT_E_INVALID;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
+    unsigned long long h[16];
+    if (hipMemcpy(h, s->stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }
 

@@ -87,7 +87,7 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
                 "rth_output_path"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_scene_last_stats",
-               "rt_scene_set_option", "rt_strerror"]
+               "rt_scene_set_option", "rt_scene_debug_counters", "rt_strerror"]
 
 
 def host_lib() -> C.CDLL:
@@ -140,6 +140,7 @@ def hip_lib() -> C.CDLL:
                                                  C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                                  C.c_void_p]
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
+        L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
         L.rt_strerror.restype = C.c_char_p
@@ -298,6 +299,12 @@ class GpuScene:
         st = rt_stats()
         _check(hip_lib().rt_scene_last_stats(self._h, C.byref(st)), "rt_scene_last_stats")
         return st
+
+    def debug_counters(self) -> list[int]:
+        """Raw device counters of the last render (rt_scene_debug_counters)."""
+        buf = (C.c_ulonglong * 16)()
+        _check(hip_lib().rt_scene_debug_counters(self._h, buf, 16), "rt_scene_debug_counters")
+        return list(buf)
 
 
 def render_scene(path: str, cwd: str | None = None, device: int = 0, depth: int | None = None,
