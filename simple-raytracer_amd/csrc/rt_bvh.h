@@ -145,6 +145,43 @@ inline void collapse4(const Result &R, Result4 &Q) {
     Q.nodes[0].max_stack = Q.max_stack;
 }
 
+// Leaf record stream: the device reads a leaf's primitives from one
+// contiguous run of 16-B words (no key indirection, one batch of loads per
+// primitive).  Rewrites every leaf link of Q (encoded against `keys` as
+// leaf_link) to
+//     -(1 + (off << 8 | nfaces << 4 | count)),   off in 16-B words, < 2^23
+// with the leaf's faces first, then its spheres (each group in key order).
+// is_face(key) tells the kind; emit(key) appends the primitive's words and
+// returns how many it appended.  Returns false if `off` outgrows its field.
+inline void leaf_decode(int32_t link, int &off, int &nfaces, int &count) {
+    int v = -link - 1;
+    off = v >> 8;
+    nfaces = (v >> 4) & 15;
+    count = v & 15;
+}
+template <class IsFace, class Emit>
+inline bool leaf_records(Result4 &Q, const std::vector<int32_t> &keys, IsFace is_face, Emit emit) {
+    size_t words = 0;
+    for (Node4 &n : Q.nodes) {
+        for (int i = 0; i < 4; i++) {
+            int32_t l = n.link[i];
+            if (l >= 0 || l == kEmpty) continue;
+            int v = -l - 1, first = v >> 4, count = v & 15;
+            std::vector<int32_t> ks(keys.begin() + first, keys.begin() + first + count);
+            std::stable_sort(ks.begin(), ks.end(), [&](int32_t a, int32_t b) {
+                bool fa = is_face(a), fb = is_face(b);
+                return fa != fb ? fa : a < b;
+            });
+            int nfaces = 0;
+            for (int32_t k : ks) nfaces += is_face(k) ? 1 : 0;
+            if (words >= (size_t(1) << 23)) return false;
+            n.link[i] = -(1 + (int32_t)((words << 8) | (size_t)(nfaces << 4) | (size_t)count));
+            for (int32_t k : ks) words += (size_t)emit(k);
+        }
+    }
+    return true;
+}
+
 class Builder {
    public:
     static constexpr int kBins = 32;

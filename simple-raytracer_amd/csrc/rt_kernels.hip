@@ -144,7 +144,7 @@ struct Params {
     unsigned int total;                  // W * rows
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
-    const int *__restrict__ bkeys;
+    const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int susp_lanes;                      // BVH: suspend a trace when fewer lanes than this still traverse
@@ -208,7 +208,8 @@ __device__ __forceinline__ bool face_test(float4 f0, float4 f1, float4 f2, float
                                           float &t, float &a, float &b, float &g) {
     V3 n = {f1.x, f1.y, f1.z};
     float dem = vdot(n, d);
-    if (dem == 0.0f) return false;
+    // branch-free: dem == 0 (ray parallel to the plane) still means no hit,
+    // but every load of the face is needed up front (one batch per test)
     V3 v0 = {f0.x, f0.y, f0.z};
     t = -(vdot(n, o) + f0.w) / dem;
     V3 ep = vsub(vadd(o, vmul(d, t)), v0);
@@ -218,7 +219,7 @@ __device__ __forceinline__ bool face_test(float4 f0, float4 f1, float4 f2, float
     b = (d22 * d1p - d12 * d2p) / det;
     g = (d11 * d2p - d12 * d1p) / det;
     a = 1.0f - (b + g);
-    return (0.0f < a) & (a < 1.0f) & (0.0f < b) & (b < 1.0f) & (0.0f < g) & (g < 1.0f);
+    return (dem != 0.0f) & (0.0f < a) & (a < 1.0f) & (0.0f < b) & (b < 1.0f) & (0.0f < g) & (g < 1.0f);
 }
 
 // TraceRay's sphere test (main.cpp:1225-1258): both roots, A = 1 assumed.
@@ -378,20 +379,37 @@ __device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
                 continue;
             }
         } else {
+            // leaf: faces (5 words each) then spheres (2 words), rt_bvh.h leaf_records
             int v = -node - 1;
-            int first = v >> 4, count = v & 15;
-            for (int k = first; k < first + count; k++) {
-                int key = p.bkeys[k];
+            const float4 *R = p.leafrec + (v >> 8);
+            int nfc = (v >> 4) & 15, count = v & 15;
+            for (int k = 0; k < count; k++) {
                 float t[2];
                 int nt = 0;
-                if (key < p.nf) {
-                    const float4 *F = p.fscan + 5 * key;
+                int key;
+                float fac;
+                // one batch of loads for either kind (a sphere reads 3 words
+                // past its record; the stream is padded for the last one)
+                const f4v *RV = reinterpret_cast<const f4v *>(R);
+                f4v w0 = RV[0], w1 = RV[1], w2 = RV[2], w3 = RV[3], w4 = RV[4];
+                asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
+                float4 f0 = make_float4(w0.x, w0.y, w0.z, w0.w), f1 = make_float4(w1.x, w1.y, w1.z, w1.w);
+                float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
+                float4 f4 = make_float4(w4.x, w4.y, w4.z, w4.w);
+                if (k < nfc) {
+                    R += 5;
+                    key = __float_as_int(f4.y);
+                    fac = f4.z;
                     float a, bb, g;
                     cnt.ftests++;
-                    if (F[1].w != 0.0f && face_test(F[0], F[1], F[2], F[3], F[4], q.o, q.d, t[0], a, bb, g)) nt = 1;
+                    if (face_test(f0, f1, f2, f3, f4, q.o, q.d, t[0], a, bb, g) & (f1.w != 0.0f)) nt = 1;
                 } else {
+                    float4 sc = f0, e = f1;
+                    R += 2;
+                    key = __float_as_int(e.x);
+                    fac = e.y;
                     cnt.stests++;
-                    if (sphere_test(p.sscan[key - p.nf], q.o, q.d, t[0], t[1])) nt = 2;
+                    if (sphere_test(sc, q.o, q.d, t[0], t[1])) nt = 2;
                 }
                 for (int r = 0; r < nt; r++) {
                     float tt = t[r];
@@ -403,8 +421,7 @@ __device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
                             win = key;
                         }
                     } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
-                        float f = cst(p.ofac)[key];
-                        if (f == 0.0f && p.shadow_early_out) {
+                        if (fac == 0.0f && p.shadow_early_out) {
                             opaque = true;
                         } else if (nh < kHits) {
                             hits[nh * kBlock] = key;
@@ -1040,7 +1057,9 @@ struct rt_scene {
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
-    int *d_bkeys = nullptr;
+    float4 *d_leafrec = nullptr;
+    std::vector<float4> h_fscan, h_sscan;   // host copies for the leaf records
+    std::vector<float> h_ofac;
     int bvh_depth = 0;
     int bvh_stack = 0;
     bool bvh_ok = false;
@@ -1155,21 +1174,42 @@ int build_bvh(rt_scene *s, double D) {
     if (ok && !R.nodes.empty()) rtbvh::collapse4(R, Q);
     s->bvh_depth = Q.depth;
     s->bvh_stack = Q.max_stack;
+    // leaf records: face = its 5 scan words with (key, shadow factor) in the
+    // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
+    std::vector<float4> rec;
+    const int nf = s->base.nf;
+    if (ok && !Q.nodes.empty())
+        ok = rtbvh::leaf_records(Q, R.keys, [nf](int32_t k) { return k < nf; }, [&](int32_t k) {
+            float kb;
+            memcpy(&kb, &k, sizeof kb);
+            float fac = s->h_ofac[k];
+            if (k < nf) {
+                for (int j = 0; j < 5; j++) rec.push_back(s->h_fscan[5 * (size_t)k + j]);
+                rec.back().y = kb;
+                rec.back().z = fac;
+                return 5;
+            }
+            rec.push_back(s->h_sscan[k - nf]);
+            rec.push_back(make_float4(kb, fac, 0.0f, 0.0f));
+            return 2;
+        });
+    rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
     // the device stack holds kStack entries: a deeper tree uses the scan
     s->bvh_ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
     s->bvh_D = D;
     if (!s->bvh_ok) return RT_OK;                              // fall back to the scan
     if (s->d_bvh) (void)hipFree(s->d_bvh);
-    if (s->d_bkeys) (void)hipFree(s->d_bkeys);
+    if (s->d_leafrec) (void)hipFree(s->d_leafrec);
     s->d_bvh = nullptr;
-    s->d_bkeys = nullptr;
+    s->d_leafrec = nullptr;
     if (hipMalloc(&s->d_bvh, Q.nodes.size() * sizeof(rtbvh::Node4)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMalloc(&s->d_bkeys, R.keys.size() * sizeof(int)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&s->d_leafrec, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess) return RT_E_NOMEM;
     if (hipMemcpy(s->d_bvh, Q.nodes.data(), Q.nodes.size() * sizeof(rtbvh::Node4), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s->d_bkeys, R.keys.data(), R.keys.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+        (!rec.empty() &&
+         hipMemcpy(s->d_leafrec, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess))
         return RT_E_HIP;
     s->base.bvh = s->d_bvh;
-    s->base.bkeys = s->d_bkeys;
+    s->base.leafrec = s->d_leafrec;
     return RT_OK;
 }
 
@@ -1188,7 +1228,7 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
         if (s->bvh_ok) {
             mode = MODE_BVH;
             p.bvh = s->base.bvh;
-            p.bkeys = s->base.bkeys;
+            p.leafrec = s->base.leafrec;
         }
     }
     if (mode == MODE_SCAN) {
@@ -1321,6 +1361,9 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
         if (!(s->scene_lo[k] <= s->scene_hi[k])) s->scene_lo[k] = s->scene_hi[k] = 0.0f;
     bool nan_fac = false;
     for (float f : ofac) nan_fac |= std::isnan(f);
+    s->h_fscan = fscan;
+    s->h_sscan = sscan;
+    s->h_ofac = ofac;
     std::vector<LightK> lights((size_t)desc->n_lights);
     for (int i = 0; i < desc->n_lights; i++) {
         const rt_light_desc &L = desc->lights[i];
@@ -1389,7 +1432,7 @@ int rt_scene_destroy(rt_scene *s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (void *d : s->allocs) (void)hipFree(d);
     if (s->d_bvh) (void)hipFree(s->d_bvh);
-    if (s->d_bkeys) (void)hipFree(s->d_bkeys);
+    if (s->d_leafrec) (void)hipFree(s->d_leafrec);
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);

@@ -112,6 +112,44 @@ int main(int argc, char **argv) {
     }
     if (cov4 != n) { printf("FAIL covered4 %d of %d\n", cov4, n); return 1; }
     if (maxstack > Q.max_stack || Q.nodes[0].max_stack != Q.max_stack) { printf("FAIL max_stack\n"); return 1; }
+    // leaf record stream: same keys per leaf, faces first, contiguous words
+    {
+        Result4 Q2 = Q;
+        std::vector<int> words;   // one int per 16-B word: the key of its primitive
+        auto is_face = [](int32_t k) { return k % 3 == 0; };
+        bool ok = leaf_records(Q2, R.keys, is_face, [&](int32_t k) {
+            int w = is_face(k) ? 5 : 2;
+            for (int j = 0; j < w; j++) words.push_back(k);
+            return w;
+        });
+        if (!ok) { printf("FAIL leaf_records\n"); return 1; }
+        int seen = 0;
+        for (size_t ni = 0; ni < Q.nodes.size(); ni++)
+            for (int i = 0; i < 4; i++) {
+                int32_t a = Q.nodes[ni].link[i], b = Q2.nodes[ni].link[i];
+                if (a >= 0 || a == kEmpty) {
+                    if (a != b) { printf("FAIL leaf_records inner link\n"); return 1; }
+                    continue;
+                }
+                int v = -a - 1, first = v >> 4, count = v & 15;
+                int off, nfc, cnt;
+                leaf_decode(b, off, nfc, cnt);
+                if (cnt != count) { printf("FAIL leaf_records count\n"); return 1; }
+                std::vector<int> want(R.keys.begin() + first, R.keys.begin() + first + count), got;
+                int w = off;
+                for (int q = 0; q < cnt; q++) {
+                    int k = words.at(w);
+                    if ((q < nfc) != is_face(k)) { printf("FAIL leaf_records order\n"); return 1; }
+                    got.push_back(k);
+                    w += is_face(k) ? 5 : 2;
+                }
+                std::sort(want.begin(), want.end());
+                std::sort(got.begin(), got.end());
+                if (want != got) { printf("FAIL leaf_records keys\n"); return 1; }
+                seen += cnt;
+            }
+        if (seen != n) { printf("FAIL leaf_records coverage\n"); return 1; }
+    }
     printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d nodes4=%zu depth4=%d stack4=%d\n", n,
            R.nodes.size(), leaves, R.depth, maxd, Q.nodes.size(), Q.depth, Q.max_stack);
     return 0;
