@@ -27,7 +27,8 @@ for f in sorted(glob.glob(os.path.join(base, "p*", "run_kernel_trace.csv"))):
     for row in csv.DictReader(open(f)):
         if KERNEL in row["Kernel_Name"]:
             dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-out = {"kernel": KERNEL, "per_render": per, "kernel_ns_per_render": sum(dur) / renders, "dispatches": len(dur)}
+# every pass is its own run of the same render(s): mean duration per dispatch
+out = {"kernel": KERNEL, "per_render": per, "kernel_ns_mean": sum(dur) / max(1, len(dur)), "dispatches": len(dur)}
 g = lambda k: per.get(k, float("nan"))
 d = {}
 d["valu_inst_per_wave"] = g("SQ_INSTS_VALU") / g("SQ_WAVES")
