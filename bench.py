@@ -199,7 +199,9 @@ def main() -> None:
         px = nrows * W
         scene_bytes = 80 * nt + 16 * ns + 52 * (ns + nt)
         alg_bytes = 12 * px + scene_bytes
-        traffic = load_pmc_traffic(args.config)
+        # PMC bytes were collected for a whole-image launch: only the N=1 line's
+        # launch is that launch (a rank's strip at N>1 is not measured)
+        traffic = load_pmc_traffic(args.config) if world == 1 else None
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             def gpu_rays(p):
