@@ -147,8 +147,6 @@ struct Params {
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
-    int susp_lanes;                      // BVH: suspend a trace when fewer lanes than this still traverse
-    int susp_iter;                       //      ... and the lane made at least this many steps (0 = never)
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -177,7 +175,6 @@ struct Query {
     bool closest, unb, skipchk, skipped;
     bool bf;                              // BVH mode: this query needs the brute-force scan
     C3 mask;
-    int trav;                             // BVH mode: 0 fresh, else suspended trace (sp | nh << 8)
 };
 
 constexpr float kInf = __builtin_huge_valf();
@@ -310,33 +307,98 @@ __device__ __forceinline__ void slab(float lx, float ly, float lz, float hx, flo
     tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
 }
 
+// One leaf's primitives against q: faces (5 words each) then spheres (2 words),
+// rt_bvh.h leaf_records.  Closest: running (best, win); shadow: valid hits go
+// to the lane's LDS key list (opaque -> early out, > kHits -> brute force).
+__device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, int *hits, Counters &cnt,
+                                           float &best, int &win, int &nh, bool &opaque) {
+    int v = -link - 1;
+    const float4 *R = p.leafrec + (v >> 8);
+    int nfc = (v >> 4) & 15, count = v & 15;
+    for (int k = 0; k < count; k++) {
+        float t[2];
+        int nt = 0;
+        int key;
+        float fac;
+        // one batch of loads for either kind (a sphere reads 3 words past its
+        // record; the stream is padded for the last one)
+        const f4v *RV = reinterpret_cast<const f4v *>(R);
+        f4v w0 = RV[0], w1 = RV[1], w2 = RV[2], w3 = RV[3], w4 = RV[4];
+        asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
+        float4 f0 = make_float4(w0.x, w0.y, w0.z, w0.w), f1 = make_float4(w1.x, w1.y, w1.z, w1.w);
+        float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
+        float4 f4 = make_float4(w4.x, w4.y, w4.z, w4.w);
+        if (k < nfc) {
+            R += 5;
+            key = __float_as_int(f4.y);
+            fac = f4.z;
+            float a, bb, g;
+            cnt.ftests++;
+            if (face_test(f0, f1, f2, f3, f4, q.o, q.d, t[0], a, bb, g) & (f1.w != 0.0f)) nt = 1;
+        } else {
+            R += 2;
+            key = __float_as_int(f1.x);
+            fac = f1.y;
+            cnt.stests++;
+            if (sphere_test(f0, q.o, q.d, t[0], t[1])) nt = 2;
+        }
+        for (int r = 0; r < nt; r++) {
+            float tt = t[r];
+            if (q.closest) {
+                bool valid = (tt > q.tmin) & (tt < kFltMax);
+                bool better = (tt < best) | ((tt == best) & (key < win));
+                if (valid & better) {
+                    best = tt;
+                    win = key;
+                }
+            } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
+                if (fac == 0.0f && p.shadow_early_out) {
+                    opaque = true;
+                } else if (nh < kHits) {
+                    hits[nh * kBlock] = key;
+                    nh++;
+                } else {
+                    q.bf = true;                   // too many: let the scan redo it in order
+                }
+            }
+        }
+    }
+}
+
+#ifndef RT_TRAV
+#define RT_TRAV 1                        // 0: if-if loop, 1: while-while with postponed leaves
+#endif
+
 // stk: this lane's stack (entries kBlock apart); hits: its kHits-entry list of
 // shadow-hit object keys (also kBlock apart), both in LDS.
 //
-// Dynamic fetch (Aila & Laine 2009): once fewer than p.susp_lanes lanes of the
-// wave are still traversing, a lane that has made p.susp_iter steps suspends
-// at its next pop -- the node stays on its LDS stack, (sp, nh) go to q.trav,
-// the running closest hit to q.tmax / q.win -- so that the finished lanes can
-// shade and fetch new rays instead of idling behind the long ones.  The
-// result does not depend on where a trace is cut.  Returns true if suspended.
-__device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
+// While-while traversal with speculative leaf postponement (Aila & Laine
+// 2009): a lane that reaches a leaf parks it and keeps descending inner nodes
+// until every active lane of the wave holds a leaf; the leaves are then
+// visited together.  Node visits stay one dependent fetch each, and the leaf
+// code runs with most lanes active instead of in almost every wave trip.  The
+// result does not depend on the visiting order (module comment above).
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
     const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
-    int win = q.win;                           // -1 on a fresh closest query
-    int nh = q.trav >> 8;
+    int win = -1;
+    int nh = 0;
     bool opaque = false;
-    int sp = q.trav & 255;
-    int node = 0;
-    if (sp) node = stk[(--sp) * kBlock];
-    q.trav = 0;
-    int steps = 0;
+    int sp = 0;
+    int node = 0;                              // >= 0 inner node, < 0 leaf, kEmpty: done
+#if RT_TRAV
+    int leaf = rtbvh::kEmpty;                  // postponed leaf
     for (;;) {
-#if RT_PROF
-        cnt.trips++;
-#endif
+        while (node >= 0) {
+#else
+    for (;;) {
         if (node >= 0) {
+#endif
+#if RT_PROF
+            cnt.trips++;
+#endif
             // 4-wide node: lo.x/y/z rows, hi.x/y/z rows, links (rt_bvh.h Node4)
             const float4 *N = p.bvh + 8 * node;
             float4 lx = N[0], ly = N[1], lz = N[2], hx = N[3], hy = N[4], hz = N[5];
@@ -371,6 +433,40 @@ __device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             RT_CSWAP(k1, c1, k3, c3);
             RT_CSWAP(k1, c1, k2, c2);
 #undef RT_CSWAP
+#if RT_TRAV
+            if (k3 < kInf) stk[(sp++) * kBlock] = c3;
+            if (k2 < kInf) stk[(sp++) * kBlock] = c2;
+            if (k1 < kInf) stk[(sp++) * kBlock] = c1;
+            if (k0 < kInf) {
+                node = c0;
+            } else {
+                node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            }
+            if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
+                leaf = node;                   // park it, keep descending
+                node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            }
+            if (__ballot(leaf == rtbvh::kEmpty) == 0ull) break;   // every lane holds a leaf
+        }
+        // visit the parked leaf, then any leaf the lane stopped on
+        while (leaf != rtbvh::kEmpty) {
+#if RT_PROF
+            cnt.trips++;
+#endif
+            leaf_visit(q, p, leaf, hits, cnt, best, win, nh, opaque);
+            leaf = rtbvh::kEmpty;
+            if (opaque || q.bf) {
+                node = rtbvh::kEmpty;
+                break;
+            }
+            if (node < 0 && node != rtbvh::kEmpty) {
+                leaf = node;
+                node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            }
+        }
+        if (node == rtbvh::kEmpty) break;
+    }
+#else
             if (k0 < kInf) {
                 if (k3 < kInf) stk[(sp++) * kBlock] = c3;
                 if (k2 < kInf) stk[(sp++) * kBlock] = c2;
@@ -379,74 +475,17 @@ __device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
                 continue;
             }
         } else {
-            // leaf: faces (5 words each) then spheres (2 words), rt_bvh.h leaf_records
-            int v = -node - 1;
-            const float4 *R = p.leafrec + (v >> 8);
-            int nfc = (v >> 4) & 15, count = v & 15;
-            for (int k = 0; k < count; k++) {
-                float t[2];
-                int nt = 0;
-                int key;
-                float fac;
-                // one batch of loads for either kind (a sphere reads 3 words
-                // past its record; the stream is padded for the last one)
-                const f4v *RV = reinterpret_cast<const f4v *>(R);
-                f4v w0 = RV[0], w1 = RV[1], w2 = RV[2], w3 = RV[3], w4 = RV[4];
-                asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
-                float4 f0 = make_float4(w0.x, w0.y, w0.z, w0.w), f1 = make_float4(w1.x, w1.y, w1.z, w1.w);
-                float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
-                float4 f4 = make_float4(w4.x, w4.y, w4.z, w4.w);
-                if (k < nfc) {
-                    R += 5;
-                    key = __float_as_int(f4.y);
-                    fac = f4.z;
-                    float a, bb, g;
-                    cnt.ftests++;
-                    if (face_test(f0, f1, f2, f3, f4, q.o, q.d, t[0], a, bb, g) & (f1.w != 0.0f)) nt = 1;
-                } else {
-                    float4 sc = f0, e = f1;
-                    R += 2;
-                    key = __float_as_int(e.x);
-                    fac = e.y;
-                    cnt.stests++;
-                    if (sphere_test(sc, q.o, q.d, t[0], t[1])) nt = 2;
-                }
-                for (int r = 0; r < nt; r++) {
-                    float tt = t[r];
-                    if (q.closest) {
-                        bool valid = (tt > q.tmin) & (tt < kFltMax);
-                        bool better = (tt < best) | ((tt == best) & (key < win));
-                        if (valid & better) {
-                            best = tt;
-                            win = key;
-                        }
-                    } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
-                        if (fac == 0.0f && p.shadow_early_out) {
-                            opaque = true;
-                        } else if (nh < kHits) {
-                            hits[nh * kBlock] = key;
-                            nh++;
-                        } else {
-                            q.bf = true;           // too many: let the scan redo it in order
-                        }
-                    }
-                }
-            }
+#if RT_PROF
+            cnt.trips++;
+#endif
+            leaf_visit(q, p, node, hits, cnt, best, win, nh, opaque);
             if (opaque || q.bf) break;
         }
         if (sp == 0) break;
-        if (++steps >= p.susp_iter && p.susp_iter > 0 &&
-            __popcll(__builtin_amdgcn_read_exec()) < (unsigned)p.susp_lanes) {
-            q.trav = sp | (nh << 8);
-            if (q.closest) {
-                q.tmax = best;
-                q.win = win;
-            }
-            return true;
-        }
         sp--;
         node = stk[sp * kBlock];
     }
+#endif
     if (q.closest) {
         if (win >= 0) {
             q.tmax = best;
@@ -469,7 +508,6 @@ __device__ bool bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             for (int i = 0; i < nh; i++) q.mask = cmulf(q.mask, cst(p.ofac)[hits[i * kBlock]]);
         }
     }
-    return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -904,9 +942,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
-    bool suspended = false;    // MODE_BVH: q's trace was cut short, resume it
     int px = 0, py = 0;
-    q.trav = 0;
 #if RT_PROF
     cnt.trips = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
@@ -916,7 +952,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         unsigned long long c0 = __builtin_amdgcn_s_memtime();
 #endif
         int kind = RK_NONE;
-        if (pending && !suspended) {
+        if (pending) {
             C3 color;
             kind = advance<MAXF>(p, ls, q, cnt, color);
             pending = kind != RK_NONE;
@@ -979,7 +1015,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(pending && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (pending && !q.bf) suspended = bvh_trace(q, p, stk, hits, cnt);
+            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1450,8 +1486,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
-    else if (k == "susp") s->base.susp_lanes = (int)std::max(0LL, std::min(64LL, value));
-    else if (k == "susp_iter") s->base.susp_iter = (int)std::max(0LL, value);
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);

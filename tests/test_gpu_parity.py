@@ -55,24 +55,16 @@ def test_scene_parity(name, golden):
         assert diff_px <= MAX_BAD_FRAC, diff_px
 
 
-# (accel, susp, susp_iter): brute-force scan; BVH without suspension; BVH
-# whose traces are cut at every pop as soon as one lane of the wave is done
-# (the harshest resume schedule); BVH with a moderate schedule.
-PATHS = [(0, 0, 0), (1, 0, 0), (1, 64, 1), (1, 24, 6)]
-
-
-@pytest.mark.parametrize("path", PATHS, ids=lambda t: "accel%d_susp%d_%d" % t)
+@pytest.mark.parametrize("accel", [0, 1])
 @pytest.mark.parametrize("name", golden_names(lambda v: v["width"] * v["height"] <= 300 * 300))
-def test_scene_parity_forced_path(name, path, golden):
-    """Every search strategy on every small fixture: the brute-force scan and
-    the BVH (with its exact fallbacks, with and without suspended/resumed
-    traces), each against the oracle, with identical ray counts."""
-    accel, susp, susp_iter = path
-    img, st = rtamd.render_scene(name, cwd=SCENES,
-                                 options={"accel": accel, "susp": susp, "susp_iter": susp_iter})
+def test_scene_parity_forced_path(name, accel, golden):
+    """Both search strategies on every small fixture: the brute-force scan
+    (accel=0) and the BVH (accel=1, with its exact fallbacks), each against
+    the oracle, with identical ray counts."""
+    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel})
     ref, cnt = OracleScene(name, cwd=SCENES).render()
     c = compare(img, ref)
-    tag = "accel%d_susp%d_%d" % path
+    tag = "accel%d" % accel
     _summary[f"{name}@{tag}"] = dict(c, tests=dict(box=st.box_tests, face=st.face_tests,
                                                    sphere=st.sphere_tests))
     assert_parity(img, ref, f"{name} {tag}")
