@@ -161,9 +161,11 @@ int rt_render_row_blocks_async(rt_scene *scene, const rt_camera *cam, int W, int
  * (persistent blocks, 0 = occupancy), "depth" (recursion depth override). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
-/* Raw device counters of the last render (diagnostics): [0..8] as in
- * rt_stats, [9..15] per-wave cycle / occupancy counters of an RT_PROF build
- * (zero otherwise). n <= 16. */
+/* Raw counters of the last render (diagnostics): [0..8] as in rt_stats,
+ * [9..15] per-wave cycle / occupancy counters of an RT_PROF build (zero
+ * otherwise), then launch facts: [16] kernel mode (0 scan, 1 LDS scan, 2 BVH),
+ * [17] resident blocks per CU, [18] grid, [19] LDS bytes per block,
+ * [20] BVH nodes, [21] BVH depth, [22] BVH worst-case stack, [23] CUs. n <= 24. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

@@ -1100,6 +1100,8 @@ struct rt_scene {
     int bvh_stack = 0;
     bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
+    long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
+    long long bvh_nodes = 0;
     bool last_valid = false;
 };
 
@@ -1138,6 +1140,10 @@ hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
     long long need = ((long long)p.total + kBlock - 1) / kBlock;
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
+    s->last_blocks_per_cu = nb;
+    s->last_grid = grid;
+    s->last_lds = (long long)shm;
+    s->last_mode = MODE;
     hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, p);
     return hipGetLastError();
 }
@@ -1210,6 +1216,7 @@ int build_bvh(rt_scene *s, double D) {
     if (ok && !R.nodes.empty()) rtbvh::collapse4(R, Q);
     s->bvh_depth = Q.depth;
     s->bvh_stack = Q.max_stack;
+    s->bvh_nodes = (long long)Q.nodes.size();
     // leaf records: face = its 5 scan words with (key, shadow factor) in the
     // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
     std::vector<float4> rec;
@@ -1557,11 +1564,19 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
 }
 
 int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
-    if (!s || !out || n < 0 || n > 16 || !s->last_valid) return RT_E_INVALID;
+    if (!s || !out || n < 0 || n > 24 || !s->last_valid) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
-    unsigned long long h[16];
-    if (hipMemcpy(h, s->stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    unsigned long long h[24];
+    if (hipMemcpy(h, s->stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    h[16] = (unsigned long long)s->last_mode;
+    h[17] = (unsigned long long)s->last_blocks_per_cu;
+    h[18] = (unsigned long long)s->last_grid;
+    h[19] = (unsigned long long)s->last_lds;
+    h[20] = (unsigned long long)s->bvh_nodes;
+    h[21] = (unsigned long long)s->bvh_depth;
+    h[22] = (unsigned long long)s->bvh_stack;
+    h[23] = (unsigned long long)s->num_cu;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }

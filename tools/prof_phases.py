@@ -48,6 +48,8 @@ def main():
         "traversal_simd_eff": ltrips / (64 * wtrips) if wtrips else None,
         "lane_trips_per_trace_lane": ltrips / lanes if lanes else None,
         "wave_trips_per_iter": wtrips / iters if iters else None,
+        "launch": dict(zip(["mode", "blocks_per_cu", "grid", "lds_bytes", "bvh_nodes", "bvh_depth",
+                            "bvh_stack", "cus"], c[16:24])),
         "raw": c,
     }
     print(json.dumps(res, indent=1))
