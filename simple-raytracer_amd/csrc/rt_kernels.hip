@@ -270,15 +270,19 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 
 // ---------------------------------------------------------------------------
 // BVH traversal (MODE_BVH).  Candidates come from the BVH in any order; the
-// reference's sequential semantics are restored exactly:
+// reference's sequential semantics are restored:
 //   closest : keep the smallest t, ties -> smallest object index (= the
 //             reference's first-in-order winner under its strict '<');
-//   shadow  : valid hits are recorded and multiplied into the mask in object
-//             order (both roots of a sphere are adjacent); an opaque hit
-//             zeroes the mask whatever the order (when no factor is NaN).
+//   shadow  : every valid hit multiplies the mask.  All factors and the mask
+//             lie in [0,1] (the clamps never fire), so the product in
+//             traversal order differs from the reference's object order by
+//             rounding only (<= 1 ulp per factor); an opaque
+//             hit zeroes the mask whatever the order (early exit when no
+//             factor is NaN).  RT_ORDERED_SHADOW=1 restores the object order
+//             bit for bit with an LDS key list (kHits entries per lane).
 // Queries the BVH cannot reproduce (SKIP_TRANS checks, directional shadow
-// rays against spheres, > kHits semi-transparent shadow hits) set q.bf and are
-// re-run by the brute-force scan.
+// rays against spheres[, > kHits semi-transparent hits when ordered]) set
+// q.bf and are re-run by the brute-force scan.
 // ---------------------------------------------------------------------------
 // Per-lane counters kept small (VGPR pressure): ray kinds are counted per
 // wave with ballots in the main loop (scalar registers); only the rare events
@@ -292,7 +296,10 @@ struct Counters {
 };
 enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
-constexpr int kHits = 8;
+#ifndef RT_ORDERED_SHADOW
+#define RT_ORDERED_SHADOW 0
+#endif
+constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
 
 __device__ __forceinline__ float safe_rcp(float x) {
     return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
@@ -354,11 +361,16 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
             } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
                 if (fac == 0.0f && p.shadow_early_out) {
                     opaque = true;
+#if RT_ORDERED_SHADOW
                 } else if (nh < kHits) {
                     hits[nh * kBlock] = key;
                     nh++;
                 } else {
                     q.bf = true;                   // too many: let the scan redo it in order
+#else
+                } else {
+                    q.mask = cmulf(q.mask, fac);
+#endif
                 }
             }
         }
@@ -494,7 +506,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     } else if (!q.bf) {
         if (opaque) {
             q.mask = {0.0f, 0.0f, 0.0f};
-        } else {
+        } else if (RT_ORDERED_SHADOW) {
             // multiply in object order (insertion sort of the LDS list; nh <= kHits)
             for (int i = 1; i < nh; i++) {
                 int k = hits[i * kBlock];
