@@ -22,5 +22,9 @@ SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS
 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD
 FETCH_SIZE
 WRITE_SIZE
-TCC_HIT_sum TCC_MISS_sum}
+TCC_HIT_sum TCC_MISS_sum
+TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum
+TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum
+TCP_TOTAL_READ_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_WRITE_sum
+TA_BUSY_avr TCP_TCC_READ_REQ_LATENCY_sum}
 PASSES

@@ -40,5 +40,11 @@ d["active_frac"] = g("SQ_ACTIVE_INST_ANY") / g("SQ_WAVE_CYCLES")
 d["hbm_read_bytes_corrected"] = 2 * g("FETCH_SIZE") * 1024
 d["hbm_write_bytes"] = g("WRITE_SIZE") * 1024
 d["l2_hit_rate"] = g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum"))
+# memory-side requests that went to DRAM (the rest are served by the
+# Infinity Cache / other fabric targets)
+d["dram_read_req_frac"] = g("TCC_EA0_RDREQ_DRAM_sum") / g("TCC_EA0_RDREQ_sum")
+d["dram_write_req_frac"] = g("TCC_EA0_WRREQ_DRAM_sum") / g("TCC_EA0_WRREQ_sum")
+d["l1_read_miss_frac"] = g("TCP_TCC_READ_REQ_sum") / g("TCP_TOTAL_READ_sum")
+d["l1_to_l2_read_latency_cyc"] = g("TCP_TCC_READ_REQ_LATENCY_sum") / g("TCP_TCC_READ_REQ_sum")
 out["derived"] = d
 print(json.dumps(out, indent=1))
