@@ -640,9 +640,24 @@ __device__ __forceinline__ void light_vectors(const LightK &lt, V3 P, V3 &L, V3 
     }
 }
 
+// Specular power powf(max(0, N.H), n) (main.cpp:954): exp2(n * log2 x) on the
+// transcendental unit (v_log_f32 / v_exp_f32) instead of ocml's ~170-
+// instruction powf.  The base is in [0, 1]; relative error ~1e-6 * max(1, |n
+// log2 x|), far inside the 1e-4 parity bar on a colour term.  powf's special
+// cases that exp2/log2 would get wrong are kept: x^0 = 1 (also for NaN, 0),
+// 1^n = 1 (also for n = inf, NaN).
+__device__ __forceinline__ float spec_pow(float x, float n) {
+    if ((n == 0.0f) | (x == 1.0f)) return 1.0f;
+    return __builtin_amdgcn_exp2f(n * __builtin_amdgcn_logf(x));
+}
+
 // (float)(F_0 + (1.0 - F_0) * powf(1.0 - cos, 5.0)), main.cpp:966 / :1104
 __device__ __forceinline__ float schlick(float F0, float cosI) {
-    float p5 = powf((float)(1.0 - (double)cosI), 5.0f);
+    // powf(x, 5) as x^2^2 * x: within 2 ulp of glibc's powf, and 0 exactly
+    // when x is (the `Fr != 0` test of main.cpp:1104 keeps its outcome)
+    float x = (float)(1.0 - (double)cosI);
+    float x2 = x * x;
+    float p5 = (x2 * x2) * x;
     return (float)((double)F0 + (1.0 - (double)F0) * (double)p5);
 }
 
@@ -779,7 +794,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             const ObjK &ob = p.objs[f.obj];
             V3 H = vnorm(vadd(L, f.I));
             C3 dc = cmulf(cmulf(f.dif, ob.kd), max0(vdot(f.N, L)));
-            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), powf(max0(vdot(f.N, H)), ob.n));
+            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(f.N, H)), ob.n));
             C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
             f.acc = cadd(f.acc, cmulc(cmulc(lc, f.mask), cadd(dc, sc)));
             f.light++;
