@@ -145,6 +145,33 @@ inline void collapse4(const Result &R, Result4 &Q) {
     Q.nodes[0].max_stack = Q.max_stack;
 }
 
+// Renumber Q's nodes breadth-first (root stays 0), so that the top levels of
+// the tree are nodes [0, K) for any K: the device keeps that prefix in LDS.
+inline void bfs_order(Result4 &Q) {
+    if (Q.nodes.empty()) return;
+    std::vector<int32_t> order;          // new -> old
+    std::vector<int32_t> remap(Q.nodes.size(), -1);
+    order.push_back(0);
+    remap[0] = 0;
+    for (size_t h = 0; h < order.size(); h++) {
+        const Node4 &n = Q.nodes[order[h]];
+        for (int i = 0; i < 4; i++) {
+            int32_t l = n.link[i];
+            if (l >= 0 && remap[l] < 0) {
+                remap[l] = (int32_t)order.size();
+                order.push_back(l);
+            }
+        }
+    }
+    std::vector<Node4> out(order.size());
+    for (size_t k = 0; k < order.size(); k++) {
+        out[k] = Q.nodes[order[k]];
+        for (int i = 0; i < 4; i++)
+            if (out[k].link[i] >= 0) out[k].link[i] = remap[out[k].link[i]];
+    }
+    Q.nodes.swap(out);
+}
+
 // Leaf record stream: the device reads a leaf's primitives from one
 // contiguous run of 16-B words (no key indirection, one batch of loads per
 // primitive).  Rewrites every leaf link of Q (encoded against `keys` as

@@ -78,6 +78,7 @@ enum { ENTERING = 0, EXITING = 1 };
 // SGPRs through the scalar cache instead of 64 identical per-lane loads.
 #define RT_CONST __attribute__((address_space(4)))
 typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 f4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
 template <typename T>
 __device__ __forceinline__ const RT_CONST T *cst(const T *p) {
     return (const RT_CONST T *)p;
@@ -147,6 +148,8 @@ struct Params {
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
+    int bvh_stack;                       // BVH: LDS stack entries per lane (worst case of the tree)
+    int lds_nodes;                       // BVH: nodes [0, lds_nodes) (the top levels, BFS order) served from LDS
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -390,7 +393,7 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 // visited together.  Node visits stay one dependent fetch each, and the leaf
 // code runs with most lanes active instead of in almost every wave trip.  The
 // result does not depend on the visiting order (module comment above).
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const float4 *lnodes, Counters &cnt) {
     const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
@@ -412,9 +415,24 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             cnt.trips++;
 #endif
             // 4-wide node: lo.x/y/z rows, hi.x/y/z rows, links (rt_bvh.h Node4)
-            const float4 *N = p.bvh + 8 * node;
-            float4 lx = N[0], ly = N[1], lz = N[2], hx = N[3], hy = N[4], hz = N[5];
-            int4 lk = *reinterpret_cast<const int4 *>(N + 6);
+            // the top of the tree comes from LDS (no TA/L1 traffic), the rest
+            // from global memory; 7 float4 per node either way
+            float4 lx, ly, lz, hx, hy, hz, lkf;
+            // (address-space-typed pointers: the two paths must not be merged
+            // into one flat load)
+            if (node < p.lds_nodes) {
+                const __attribute__((address_space(3))) f4v *N =
+                    (const __attribute__((address_space(3))) f4v *)(lnodes) + 7 * node;
+                lx = f4(N[0]), ly = f4(N[1]), lz = f4(N[2]), hx = f4(N[3]), hy = f4(N[4]), hz = f4(N[5]);
+                lkf = f4(N[6]);
+            } else {
+                const __attribute__((address_space(1))) f4v *N =
+                    (const __attribute__((address_space(1))) f4v *)(p.bvh) + 8 * node;
+                lx = f4(N[0]), ly = f4(N[1]), lz = f4(N[2]), hx = f4(N[3]), hy = f4(N[4]), hz = f4(N[5]);
+                lkf = f4(N[6]);
+            }
+            int4 lk = make_int4(__float_as_int(lkf.x), __float_as_int(lkf.y), __float_as_int(lkf.z),
+                                __float_as_int(lkf.w));
             float thi = q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
             float n0, f0, n1, f1, n2, f2, n3, f3;
             slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, ix, iy, iz, ox, oy, oz, tlo, thi, n0, f0);
@@ -968,6 +986,16 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: hits[k * kBlock], k < kHits
     int *stk = hits + kHits * kBlock;                       //           stack[k * kBlock]
+    // MODE_BVH node cache after the stacks: the first lds_nodes nodes, 7 float4
+    // each (a 112-B stride spreads different nodes over the LDS banks)
+    float4 *lnodes = lds + (kHits + p.bvh_stack) * (kBlock / 4);
+    if (MODE == MODE_BVH && p.lds_nodes > 0) {
+        for (int i = threadIdx.x; i < 7 * p.lds_nodes; i += blockDim.x) {
+            int nd = i / 7, k = i - nd * 7;
+            lnodes[i] = p.bvh[8 * nd + k];
+        }
+        __syncthreads();
+    }
     Query q;
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
@@ -1045,7 +1073,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(pending && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
+            if (pending && !q.bf) bvh_trace(q, p, stk, hits, lnodes, cnt);
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1128,6 +1156,8 @@ struct rt_scene {
     std::vector<float> h_ofac;
     int bvh_depth = 0;
     int bvh_stack = 0;
+    int lds_nodes = 0;                 // BVH nodes cached in LDS per block
+    long long opt_lds_nodes = -1;      // -1 auto (fill the block's LDS share), else that many
     bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
@@ -1156,7 +1186,9 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
-    if (mode == MODE_BVH) return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int);
+    if (mode == MODE_BVH)
+        return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int) +
+               (size_t)s->lds_nodes * 7 * sizeof(float4);
     return 0;
 }
 
@@ -1243,10 +1275,22 @@ int build_bvh(rt_scene *s, double D) {
     B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
     bool ok = B.build(R);
     rtbvh::Result4 Q;
-    if (ok && !R.nodes.empty()) rtbvh::collapse4(R, Q);
+    if (ok && !R.nodes.empty()) {
+        rtbvh::collapse4(R, Q);
+        rtbvh::bfs_order(Q);                 // top levels first: the LDS node cache is a prefix
+    }
     s->bvh_depth = Q.depth;
     s->bvh_stack = Q.max_stack;
     s->bvh_nodes = (long long)Q.nodes.size();
+    // LDS node cache: what the stacks leave of the block's share of the CU's
+    // 160 KB at RT_MIN_WAVES blocks per CU
+    {
+        long long budget = (163840 / RT_MIN_WAVES) & ~1023LL;
+        long long used = (long long)(kHits + std::max(1, s->bvh_stack)) * kBlock * (long long)sizeof(int);
+        long long k = std::max(0LL, (budget - used) / (7 * (long long)sizeof(float4)));
+        if (s->opt_lds_nodes >= 0) k = s->opt_lds_nodes;
+        s->lds_nodes = (int)std::min<long long>(k, s->bvh_nodes);
+    }
     // leaf records: face = its 5 scan words with (key, shadow factor) in the
     // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
     std::vector<float4> rec;
@@ -1302,6 +1346,8 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
             mode = MODE_BVH;
             p.bvh = s->base.bvh;
             p.leafrec = s->base.leafrec;
+            p.bvh_stack = std::max(1, s->bvh_stack);
+            p.lds_nodes = s->lds_nodes;
         }
     }
     if (mode == MODE_SCAN) {
@@ -1523,6 +1569,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
+    else if (k == "lds_nodes") s->opt_lds_nodes = value < 0 ? -1 : value, s->bvh_D = -1.0;
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);

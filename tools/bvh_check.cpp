@@ -80,6 +80,24 @@ int main(int argc, char **argv) {
     // 4-wide collapse: same leaves, contained boxes, every slot valid or empty
     Result4 Q;
     collapse4(R, Q);
+    size_t n4 = Q.nodes.size();
+    bfs_order(Q);
+    {   // breadth-first: same node count, depth non-decreasing with the index
+        if (Q.nodes.size() != n4) { printf("FAIL bfs size\n"); return 1; }
+        std::vector<int> dep(n4, -1);
+        dep[0] = 0;
+        for (size_t k = 0; k < n4; k++) {
+            if (dep[k] < 0) { printf("FAIL bfs unreachable\n"); return 1; }
+            if (k > 0 && dep[k] < dep[k - 1]) { printf("FAIL bfs order\n"); return 1; }
+            for (int i = 0; i < 4; i++) {
+                int32_t l = Q.nodes[k].link[i];
+                if (l >= 0) {
+                    if (l <= (int32_t)k || dep[l] >= 0) { printf("FAIL bfs link\n"); return 1; }
+                    dep[l] = dep[k] + 1;
+                }
+            }
+        }
+    }
     struct It4 { int link; float lo[3], hi[3]; int stack; };
     std::vector<It4> s4;
     s4.push_back({0, {-inf, -inf, -inf}, {inf, inf, inf}, 0});
