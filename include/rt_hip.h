@@ -165,7 +165,10 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * [9..15] per-wave cycle / occupancy counters of an RT_PROF build (zero
  * otherwise), then launch facts: [16] kernel mode (0 scan, 1 LDS scan, 2 BVH),
  * [17] resident blocks per CU, [18] grid, [19] LDS bytes per block,
- * [20] BVH nodes, [21] BVH depth, [22] BVH worst-case stack, [23] CUs. n <= 24. */
+ * [20] BVH nodes, [21] BVH depth, [22] BVH worst-case stack, [23] CUs;
+ * RT_PROF timeline (100 MHz ticks): [24] first wave start, [25] work counter
+ * drained, [26] last wave end, [27] sum of per-wave tails, [28] sum of wave
+ * lifetimes, [29] waves.  n <= 32. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

@@ -303,6 +303,7 @@ enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY 
 #define RT_ORDERED_SHADOW 0
 #endif
 constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
+constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
     return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
@@ -1004,6 +1005,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #if RT_PROF
     cnt.trips = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
+    // timeline on the constant 100 MHz clock (comparable across CUs / XCDs)
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_drain = 0;
 #endif
     for (;;) {
 #if RT_PROF
@@ -1031,7 +1035,12 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 unsigned base = 0;
                 if (lane == leader) base = atomicAdd(p.work, n);
                 base = __shfl(base, leader);
-                if (base + n >= p.total) drained = true;
+                if (base + n >= p.total) {
+                    drained = true;
+#if RT_PROF
+                    t_drain = __builtin_amdgcn_s_memrealtime();
+#endif
+                }
                 if (!busy) {
                     unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
                     unsigned idx = base + rank;
@@ -1112,6 +1121,16 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[14], pc_wtrips);
     }
     atomicAdd(&st[15], (unsigned long long)cnt.trips);
+    if (lane == 0) {
+        unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        if (!t_drain) t_drain = t_end;
+        atomicMin(&st[24], t_start);                 // kernel start (first wave)
+        atomicMin(&st[25], t_drain);                 // work counter ran out
+        atomicMax(&st[26], t_end);                   // last wave done
+        atomicAdd(&st[27], t_end - t_drain);         // sum of per-wave tails
+        atomicAdd(&st[28], t_end - t_start);         // sum of wave lifetimes
+        atomicAdd(&st[29], 1ull);                    // waves
+    }
 #endif
 }
 
@@ -1516,7 +1535,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
     if (!rc && hipMalloc(&s->work, sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
-    if (!rc && hipMalloc(&s->stats, 16 * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
+    if (!rc && hipMalloc(&s->stats, kNStats * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
     if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
     if (!rc && (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)) rc = RT_E_HIP;
     if (!rc) {
@@ -1604,7 +1623,9 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
     p.total = (unsigned)((long long)W * nrows);
     p.out = out_rgb;
     if (hipMemsetAsync(s->work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
-    if (hipMemsetAsync(s->stats, 0, 16 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    if (hipMemsetAsync(s->stats, 0, kNStats * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    // RT_PROF timeline minima start at all-ones
+    if (hipMemsetAsync(s->stats + 24, 0xff, 2 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
     (void)hipEventRecord(s->ev0, st);
     int rc = launch(s, p, st);
     (void)hipEventRecord(s->ev1, st);
@@ -1642,11 +1663,12 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
 }
 
 int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
-    if (!s || !out || n < 0 || n > 24 || !s->last_valid) return RT_E_INVALID;
+    if (!s || !out || n < 0 || n > kNStats || !s->last_valid) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
-    unsigned long long h[24];
-    if (hipMemcpy(h, s->stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    unsigned long long h[kNStats];
+    if (hipMemcpy(h, s->stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return RT_E_HIP;
     h[16] = (unsigned long long)s->last_mode;
     h[17] = (unsigned long long)s->last_blocks_per_cu;
     h[18] = (unsigned long long)s->last_grid;

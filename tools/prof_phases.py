@@ -23,8 +23,14 @@ def main():
     import rtamd
     from rtamd import scenes as gen
 
-    cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
-    opts = dict(a.split("=") for a in sys.argv[2:])
+    args = sys.argv[1:]
+    rows = None                       # --rows N:r -> rank r's row set of N (multi-GPU share)
+    if "--rows" in args:
+        i = args.index("--rows")
+        rows = tuple(int(v) for v in args[i + 1].split(":"))
+        del args[i:i + 2]
+    cfg = args[0] if args else "C3"
+    opts = dict(a.split("=") for a in args[1:])
     d = tempfile.mkdtemp(prefix="rtprof_")
     path = gen.write_scene(d, cfg)
     hs = rtamd.HostScene(path, cwd=d)
@@ -34,14 +40,19 @@ def main():
     W, H = hs.width, hs.height
     cam = hs.camera()
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    from rtamd.dist import row_set
     for _ in range(2):
-        gs.render_rows_async(cam, W, H, 0, H, out.data_ptr())
+        if rows:
+            y0, b, step, nr, _ = row_set(H, rows[0], rows[1])
+            gs.render_row_blocks_async(cam, W, H, y0, b, step, nr, out.data_ptr())
+        else:
+            gs.render_rows_async(cam, W, H, 0, H, out.data_ptr())
         st = gs.last_stats()
     c = gs.debug_counters()
     shade, trace, bf, iters, lanes, wtrips, ltrips = c[9:16]
     tot = shade + trace + bf
     res = {
-        "config": cfg, "options": opts, "kernel_ms": st.kernel_ms,
+        "config": cfg, "rows": rows, "options": opts, "kernel_ms": st.kernel_ms,
         "cycles_split": {"shade_refill": shade / tot, "trace": trace / tot, "bf_scan": bf / tot} if tot else None,
         "outer_iterations": iters,
         "trace_lane_occupancy": lanes / (64 * iters) if iters else None,
@@ -50,6 +61,10 @@ def main():
         "wave_trips_per_iter": wtrips / iters if iters else None,
         "launch": dict(zip(["mode", "blocks_per_cu", "grid", "lds_bytes", "bvh_nodes", "bvh_depth",
                             "bvh_stack", "cus"], c[16:24])),
+        "timeline_us": ({"kernel": (c[26] - c[24]) / 100.0, "drain": (c[25] - c[24]) / 100.0,
+                         "tail": (c[26] - c[25]) / 100.0, "mean_wave_tail": c[27] / max(1, c[29]) / 100.0,
+                         "mean_wave_life": c[28] / max(1, c[29]) / 100.0, "waves": c[29]}
+                        if c[29] else None),
         "raw": c,
     }
     print(json.dumps(res, indent=1))
