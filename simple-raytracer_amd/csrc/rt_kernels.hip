@@ -142,10 +142,7 @@ struct Params {
     float eye[3], ul[3], dh[3], dv[3];
     int W, y0, rows;                     // render `rows` rows of a W-wide image: local row r is
     int rblock, rstep;                   // image row y0 + (r / rblock) * rstep + r % rblock
-    unsigned int total;                  // work slots: W * rows, or 64 x tiles when tile-ordered
-    unsigned int npx;                    // W * rows
-    const unsigned *__restrict__ torder; // tile order (64-pixel tiles, costliest first), or null
-    unsigned *__restrict__ tcost;        // sample pass: per-tile cost (rays of the sampled pixel)
+    unsigned int total;                  // W * rows
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
@@ -971,9 +968,7 @@ __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, 
     y = (int)s * 8 + (int)(r % (unsigned)sh);
 }
 
-// SAMPLE: the cost pass of tile ordering -- slot t renders one pixel of tile t
-// (its full ShadeRay tree) and writes the number of rays it took to tcost[t].
-template <int MAXF, int MODE, bool SAMPLE>
+template <int MAXF, int MODE>
 __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) {
     constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
     extern __shared__ float4 lds[];
@@ -1007,7 +1002,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
     int px = 0, py = 0;
-    unsigned sslot = 0, nray = 0;             // SAMPLE: tile being costed, rays so far
 #if RT_PROF
     cnt.trips = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
@@ -1024,16 +1018,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             C3 color;
             kind = advance<MAXF>(p, ls, q, cnt, color);
             pending = kind != RK_NONE;
-            if (SAMPLE) nray += pending ? 1u : 0u;
             if (!pending) {
-                if (SAMPLE) {
-                    p.tcost[sslot] = nray;
-                } else {
-                    float *o = p.out + ((size_t)py * p.W + px) * 3;
-                    o[0] = color.r;
-                    o[1] = color.g;
-                    o[2] = color.b;
-                }
+                float *o = p.out + ((size_t)py * p.W + px) * 3;
+                o[0] = color.r;
+                o[1] = color.g;
+                o[2] = color.b;
                 busy = false;
             }
         }
@@ -1054,16 +1043,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 }
                 if (!busy) {
                     unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
-                    unsigned slot = base + rank;
-                    unsigned idx = slot;
-                    if (SAMPLE) {
-                        idx = min(slot * 64u + 36u, p.npx - 1u);
-                        sslot = slot;
-                        nray = 1;
-                    } else if (p.torder && slot < p.total) {
-                        idx = p.torder[slot >> 6] * 64u + (slot & 63u);
-                    }
-                    if (slot < p.total && idx < p.npx) {
+                    unsigned idx = base + rank;
+                    if (idx < p.total) {
                         pixel_xy(p, idx, px, py);
                         V3 pt = vadd(vadd(V3{p.ul[0], p.ul[1], p.ul[2]}, vmul(V3{p.dh[0], p.dh[1], p.dh[2]}, (float)px)),
                                      vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)image_row(p, py)));
@@ -1153,36 +1134,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #endif
 }
 
-// Tile order: counting sort of the sampled tile costs, costliest first
-// (256 buckets; the order inside a bucket is whatever the atomics give --
-// results do not depend on it).  hist[0..255] counts, hist[256..511] cursors.
-__global__ void tile_hist(const unsigned *__restrict__ cost, unsigned n, unsigned *__restrict__ hist) {
-    for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
-        atomicAdd(&hist[255u - min(cost[t], 255u)], 1u);
-}
-
-__global__ void __launch_bounds__(256) tile_scan(unsigned *__restrict__ hist) {
-    __shared__ unsigned v[256];
-    unsigned i = threadIdx.x;
-    v[i] = hist[i];
-    __syncthreads();
-    for (unsigned d = 1; d < 256; d <<= 1) {
-        unsigned x = i >= d ? v[i - d] : 0u;
-        __syncthreads();
-        v[i] += x;
-        __syncthreads();
-    }
-    hist[256 + i] = v[i] - hist[i];          // exclusive prefix = bucket start
-}
-
-__global__ void tile_scatter(const unsigned *__restrict__ cost, unsigned n, unsigned *__restrict__ hist,
-                             unsigned *__restrict__ order) {
-    for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-        unsigned pos = atomicAdd(&hist[256u + 255u - min(cost[t], 255u)], 1u);
-        order[pos] = t;
-    }
-}
-
 }  // namespace rt
 
 // ===========================================================================
@@ -1198,12 +1149,8 @@ struct rt_scene {
     std::vector<void *> allocs;
     float *dev_out = nullptr;          // staging buffer when the caller passes host memory
     size_t dev_out_bytes = 0;
-    unsigned int *work = nullptr;      // [0] render, [1] tile-order sample pass
+    unsigned int *work = nullptr;
     unsigned long long *stats = nullptr;
-    unsigned long long *sstats = nullptr;   // sample pass counters (kept out of the render's)
-    unsigned *d_tcost = nullptr, *d_torder = nullptr, *d_thist = nullptr;
-    unsigned tile_cap = 0;
-    long long opt_tile_order = -1;     // -1 auto (BVH mode, >= 64K pixels), 0 off, 1 on
     int num_cu = 0;
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
@@ -1265,76 +1212,27 @@ size_t mode_lds_bytes(const rt_scene *s, int mode) {
     return 0;
 }
 
-template <int MAXF, int MODE, bool SAMPLE = false>
+template <int MAXF, int MODE>
 hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
     size_t shm = mode_lds_bytes(s, MODE);
     int nb = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE, SAMPLE>, kBlock, shm);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE>, kBlock, shm);
     if (nb < 1) nb = 1;
     long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu;
     long long need = ((long long)p.total + kBlock - 1) / kBlock;
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
-    if (!SAMPLE) {
-        s->last_blocks_per_cu = nb;
-        s->last_grid = grid;
-        s->last_lds = (long long)shm;
-        s->last_mode = MODE;
-    }
-    hipLaunchKernelGGL((render_kernel<MAXF, MODE, SAMPLE>), dim3((unsigned)grid), dim3(kBlock), shm, st, p);
+    s->last_blocks_per_cu = nb;
+    s->last_grid = grid;
+    s->last_lds = (long long)shm;
+    s->last_mode = MODE;
+    hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, p);
     return hipGetLastError();
 }
 
-// Tile ordering (BVH mode): a sample pass prices every 64-pixel tile by the
-// rays of one of its pixels, a counting sort orders the tiles costliest first,
-// and the render takes whole tiles in that order -- the deepest ShadeRay trees
-// start early instead of forming the launch's tail, and a wave still gets one
-// coherent tile.  The sample pass has its own work counter and counters.
 template <int MAXF>
-hipError_t launch_tile_order(rt_scene *s, Params &p, hipStream_t st) {
-    unsigned ntiles = (p.npx + 63u) / 64u;
-    if (s->tile_cap < ntiles) {
-        if (s->d_tcost) (void)hipFree(s->d_tcost);
-        if (s->d_torder) (void)hipFree(s->d_torder);
-        s->d_tcost = s->d_torder = nullptr;
-        s->tile_cap = 0;
-        if (hipMalloc(&s->d_tcost, ntiles * sizeof(unsigned)) != hipSuccess ||
-            hipMalloc(&s->d_torder, ntiles * sizeof(unsigned)) != hipSuccess)
-            return hipErrorOutOfMemory;
-        s->tile_cap = ntiles;
-    }
-    hipError_t e;
-    if ((e = hipMemsetAsync(s->work + 1, 0, sizeof(unsigned), st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(s->sstats, 0, kNStats * sizeof(unsigned long long), st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(s->d_thist, 0, 512 * sizeof(unsigned), st)) != hipSuccess) return e;
-    Params ps = p;
-    ps.work = s->work + 1;
-    ps.stats = s->sstats;
-    ps.total = ntiles;
-    ps.torder = nullptr;
-    ps.tcost = s->d_tcost;
-    if ((e = launch_one<MAXF, MODE_BVH, true>(s, ps, st)) != hipSuccess) return e;
-    unsigned g = std::min<unsigned>((ntiles + 255u) / 256u, 1024u);
-    hipLaunchKernelGGL(tile_hist, dim3(g), dim3(256), 0, st, (const unsigned *)s->d_tcost, ntiles, s->d_thist);
-    hipLaunchKernelGGL(tile_scan, dim3(1), dim3(256), 0, st, s->d_thist);
-    hipLaunchKernelGGL(tile_scatter, dim3(g), dim3(256), 0, st, (const unsigned *)s->d_tcost, ntiles, s->d_thist,
-                       s->d_torder);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    p.torder = s->d_torder;
-    p.total = ntiles * 64u;
-    return hipSuccess;
-}
-
-template <int MAXF>
-hipError_t launch_mode(rt_scene *s, Params &p, int mode, hipStream_t st) {
-    if (mode == MODE_BVH) {
-        bool order = s->opt_tile_order == 1 || (s->opt_tile_order == -1 && p.npx >= 64u * 1024u);
-        if (order) {
-            hipError_t e = launch_tile_order<MAXF>(s, p, st);
-            if (e != hipSuccess) return e;
-        }
-        return launch_one<MAXF, MODE_BVH>(s, p, st);
-    }
+hipError_t launch_mode(rt_scene *s, const Params &p, int mode, hipStream_t st) {
+    if (mode == MODE_BVH) return launch_one<MAXF, MODE_BVH>(s, p, st);
     if (mode == MODE_SCAN_LDS) return launch_one<MAXF, MODE_SCAN_LDS>(s, p, st);
     return launch_one<MAXF, MODE_SCAN>(s, p, st);
 }
@@ -1636,9 +1534,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     if (!rc) rc = upload(s, lights, p.lights);
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
-    if (!rc && hipMalloc(&s->work, 2 * sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
-    if (!rc && hipMalloc(&s->sstats, kNStats * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
-    if (!rc && hipMalloc(&s->d_thist, 512 * sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
+    if (!rc && hipMalloc(&s->work, sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
     if (!rc && hipMalloc(&s->stats, kNStats * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
     if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
     if (!rc && (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)) rc = RT_E_HIP;
@@ -1679,10 +1575,6 @@ int rt_scene_destroy(rt_scene *s) {
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);
-    if (s->sstats) (void)hipFree(s->sstats);
-    if (s->d_thist) (void)hipFree(s->d_thist);
-    if (s->d_tcost) (void)hipFree(s->d_tcost);
-    if (s->d_torder) (void)hipFree(s->d_torder);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1697,7 +1589,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
-    else if (k == "tile_order") s->opt_tile_order = value < 0 ? -1 : (value ? 1 : 0);
     else if (k == "lds_nodes") s->opt_lds_nodes = value < 0 ? -1 : value, s->bvh_D = -1.0;
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
@@ -1730,9 +1621,6 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
     p.rblock = block;
     p.rstep = step;
     p.total = (unsigned)((long long)W * nrows);
-    p.npx = p.total;
-    p.torder = nullptr;
-    p.tcost = nullptr;
     p.out = out_rgb;
     if (hipMemsetAsync(s->work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
     if (hipMemsetAsync(s->stats, 0, kNStats * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;

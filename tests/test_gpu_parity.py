@@ -55,22 +55,16 @@ def test_scene_parity(name, golden):
         assert diff_px <= MAX_BAD_FRAC, diff_px
 
 
-# (accel, tile_order): brute-force scan; BVH in pixel order; BVH with the
-# cost-sampled tile order (forced on even for tiny images)
-PATHS = [(0, 0), (1, 0), (1, 1)]
-
-
-@pytest.mark.parametrize("path", PATHS, ids=lambda t: "accel%d_order%d" % t)
+@pytest.mark.parametrize("accel", [0, 1])
 @pytest.mark.parametrize("name", golden_names(lambda v: v["width"] * v["height"] <= 300 * 300))
-def test_scene_parity_forced_path(name, path, golden):
-    """Every search strategy on every small fixture: the brute-force scan and
-    the BVH (with its exact fallbacks, in pixel or cost-sampled tile order),
-    each against the oracle, with identical ray counts."""
-    accel, order = path
-    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel, "tile_order": order})
+def test_scene_parity_forced_path(name, accel, golden):
+    """Both search strategies on every small fixture: the brute-force scan
+    (accel=0) and the BVH (accel=1, with its exact fallbacks), each against
+    the oracle, with identical ray counts."""
+    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel})
     ref, cnt = OracleScene(name, cwd=SCENES).render()
     c = compare(img, ref)
-    tag = "accel%d_order%d" % path
+    tag = "accel%d" % accel
     _summary[f"{name}@{tag}"] = dict(c, tests=dict(box=st.box_tests, face=st.face_tests,
                                                    sphere=st.sphere_tests))
     assert_parity(img, ref, f"{name} {tag}")
@@ -172,33 +166,6 @@ def test_row_blocks_reassemble(world):
         img[image_rows(H, world, r)] = buf[:n].cpu().numpy()
     assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(full, nan=-9))
     assert rays == st.rays()
-
-
-@pytest.mark.parametrize("name", ["C3_64x64.txt", "test7_s.txt"])
-def test_tile_order_bit_identical(name):
-    """Tile ordering only changes which lane renders which pixel: the image is
-    bit-identical to the pixel-order render, and the ray counts (of the render,
-    not of the sample pass) are unchanged -- also for row sets."""
-    torch = pytest.importorskip("torch")
-    from rtamd.dist import row_set
-    hs = rtamd.HostScene(name, cwd=SCENES)
-    W, H = hs.width, hs.height
-    cam = hs.camera()
-    gs = rtamd.GpuScene(hs)
-    gs.set_option("accel", 1)
-    for world, rank in [(1, 0), (3, 1)]:
-        y0, b, step, n, per = row_set(H, world, rank)
-        imgs, rays = [], []
-        for order in (0, 1):
-            gs.set_option("tile_order", order)
-            buf = torch.full((per, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
-            gs.render_row_blocks_async(cam, W, H, y0, b, step, n, buf.data_ptr())
-            st = gs.last_stats()
-            imgs.append(np.nan_to_num(buf[:n].cpu().numpy(), nan=-9))
-            rays.append((st.primary, st.shadow, st.refraction, st.reflection, st.skip_trans, st.ub_back))
-        assert np.array_equal(imgs[0], imgs[1]), (world, rank)
-        assert rays[0] == rays[1]
-        assert rays[0][0] == n * W                   # every pixel rendered once
 
 
 def test_render_into_device_memory():
