@@ -150,6 +150,7 @@ struct Params {
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int bvh_stack;                       // BVH: LDS stack entries per lane (worst case of the tree)
     int lds_nodes;                       // BVH: nodes [0, lds_nodes) (the top levels, BFS order) served from LDS
+    void *__restrict__ frames;           // RT_GLOBAL_FRAMES: grid x kBlock x MAXF ShadeRay frames
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -770,9 +771,21 @@ __device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAX
 }
 
 // Lane state between scans.
+// RT_GLOBAL_FRAMES: the frames live in a device buffer, each lane's MAXF frames
+// contiguous (AoS per lane).  Compiler scratch interleaves lanes per dword, so
+// a store by the ~30 % of lanes active in a shading branch dirties whole
+// sectors of mostly-unchanged neighbours and the write-back traffic is ~4x the
+// bytes written; per-lane contiguous frames only dirty the lane's own sectors.
+#ifndef RT_GLOBAL_FRAMES
+#define RT_GLOBAL_FRAMES 1
+#endif
 template <int MAXF>
 struct LaneState {
+#if RT_GLOBAL_FRAMES
+    Frame<MAXF> *fr;                 // this lane's frames in Params::frames
+#else
     Frame<MAXF> fr[MAXF];
+#endif
     int top;                         // -1: primary ray pending
 };
 
@@ -983,6 +996,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
+#if RT_GLOBAL_FRAMES
+    ls.fr = reinterpret_cast<Frame<MAXF> *>(p.frames) + ((size_t)blockIdx.x * kBlock + threadIdx.x) * MAXF;
+#endif
     Counters cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: hits[k * kBlock], k < kHits
@@ -1151,6 +1167,8 @@ struct rt_scene {
     size_t dev_out_bytes = 0;
     unsigned int *work = nullptr;
     unsigned long long *stats = nullptr;
+    void *d_frames = nullptr;          // RT_GLOBAL_FRAMES buffer
+    size_t frames_cap = 0;
     int num_cu = 0;
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
@@ -1222,11 +1240,23 @@ hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
     long long need = ((long long)p.total + kBlock - 1) / kBlock;
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
+    Params pl = p;
+#if RT_GLOBAL_FRAMES
+    size_t fbytes = (size_t)grid * kBlock * MAXF * sizeof(Frame<MAXF>);
+    if (s->frames_cap < fbytes) {
+        if (s->d_frames) (void)hipFree(s->d_frames);
+        s->d_frames = nullptr;
+        s->frames_cap = 0;
+        if (hipMalloc(&s->d_frames, fbytes) != hipSuccess) return hipErrorOutOfMemory;
+        s->frames_cap = fbytes;
+    }
+    pl.frames = s->d_frames;
+#endif
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
     s->last_lds = (long long)shm;
     s->last_mode = MODE;
-    hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, p);
+    hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, pl);
     return hipGetLastError();
 }
 
@@ -1575,6 +1605,7 @@ int rt_scene_destroy(rt_scene *s) {
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->work) (void)hipFree(s->work);
     if (s->stats) (void)hipFree(s->stats);
+    if (s->d_frames) (void)hipFree(s->d_frames);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
