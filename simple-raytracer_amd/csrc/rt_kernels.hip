@@ -798,6 +798,10 @@ template <int MAXF>
 __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
     int top = ls.top;
+    // a closest hit opens frame `top` (primary hit, refraction or reflection
+    // child); its ShadeRay prologue runs at ONE call site below, so a wave
+    // whose lanes open frames for different reasons runs it once
+    bool begin = false;
     // ---- consume the scan result ----
     if (top < 0) {                                   // primary (main.cpp:729-758)
         if (q.win < 0) {
@@ -812,7 +816,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         f.stack[0] = q.win;
         f.state = ENTERING;
         f.depth = p.depth;
-        node_begin(p, f, q.o, q.d, q.tmax);
+        begin = true;
         top = 0;
     } else {
         Frame<MAXF> &f = ls.fr[top];
@@ -844,7 +848,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 c.obj = q.win;
                 c.depth = f.depth - 1;
                 f.phase = PH_REFR_CHILD;
-                node_begin(p, c, q.o, q.d, q.tmax);
+                begin = true;
                 top++;
             } else {
                 C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)ob.opacity));
@@ -858,7 +862,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 c.obj = q.win;
                 c.depth = f.depth - 1;
                 f.phase = PH_REFL_CHILD;
-                node_begin(p, c, q.o, q.d, q.tmax);
+                begin = true;
                 top++;
             } else {
                 // miss: refl = bkg * F_r; finish this node below
@@ -870,6 +874,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             }
         }
     }
+    if (begin) node_begin(p, ls.fr[top], q.o, q.d, q.tmax);
     // ---- run the current frame forward ----
     for (;;) {
         Frame<MAXF> &f = ls.fr[top];
