@@ -297,6 +297,9 @@ struct Counters {
 #if RT_PROF
     unsigned trips;                             // traversal loop iterations of this lane
 #endif
+#if RT_PROF >= 2
+    unsigned long long t_fetch, t_trip;         // inner-node trips: cycles to node data, whole trip
+#endif
 };
 enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
@@ -416,6 +419,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
 #if RT_PROF
             cnt.trips++;
 #endif
+#if RT_PROF >= 2
+            const unsigned long long t_a = __builtin_amdgcn_s_memtime();
+#endif
             // 4-wide node: lo.x/y/z rows, hi.x/y/z rows, links (rt_bvh.h Node4)
             // the top of the tree comes from LDS (no TA/L1 traffic), the rest
             // from global memory; 7 float4 per node either way
@@ -435,6 +441,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
             }
             int4 lk = make_int4(__float_as_int(lkf.x), __float_as_int(lkf.y), __float_as_int(lkf.z),
                                 __float_as_int(lkf.w));
+#if RT_PROF >= 2
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(lkf.w), "v"(lx.x), "v"(hz.w) : "memory");
+            cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
+#endif
             float thi = q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
             float n0, f0, n1, f1, n2, f2, n3, f3;
             slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, ix, iy, iz, ox, oy, oz, tlo, thi, n0, f0);
@@ -478,6 +488,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
                 leaf = node;                   // park it, keep descending
                 node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
             }
+#if RT_PROF >= 2
+            cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
+#endif
             if (__ballot(leaf == rtbvh::kEmpty) == 0ull) break;   // every lane holds a leaf
         }
         // visit the parked leaf, then any leaf the lane stopped on
@@ -547,15 +560,70 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
 // ---------------------------------------------------------------------------
 enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4 };
 
+// RT_GLOBAL_FRAMES: the frames live in a device buffer, each lane's MAXF frames
+// contiguous (AoS per lane) -- see LaneState.  RT_FRAME_NT: every frame field
+// is read and written with non-temporal accesses, which bypass the 32 KiB L1
+// (MI355X_MICROARCH.md, L1 bypass): a frame is written at one shade node and
+// read back after a trace, never reused from L1, and streaming it through L1
+// evicted the BVH nodes the next traversal needs.
+#ifndef RT_GLOBAL_FRAMES
+#define RT_GLOBAL_FRAMES 1
+#endif
+#ifndef RT_FRAME_NT
+#define RT_FRAME_NT RT_GLOBAL_FRAMES
+#endif
+template <typename T>
+struct NTf {
+    T v;
+    __device__ __forceinline__ operator T() const { return __builtin_nontemporal_load(&v); }
+    __device__ __forceinline__ NTf &operator=(T x) {
+        __builtin_nontemporal_store(x, &v);
+        return *this;
+    }
+    __device__ __forceinline__ NTf &operator=(const NTf &o) { return *this = (T)o; }
+    __device__ __forceinline__ T operator++(int) {
+        T t = *this;
+        *this = t + 1;
+        return t;
+    }
+};
+struct NTV3 {
+    NTf<float> x, y, z;
+    __device__ __forceinline__ operator V3() const { return {x, y, z}; }
+    __device__ __forceinline__ NTV3 &operator=(V3 a) {
+        x = a.x, y = a.y, z = a.z;
+        return *this;
+    }
+};
+struct NTC3 {
+    NTf<float> r, g, b;
+    __device__ __forceinline__ operator C3() const { return {r, g, b}; }
+    __device__ __forceinline__ NTC3 &operator=(C3 a) {
+        r = a.r, g = a.g, b = a.b;
+        return *this;
+    }
+};
+#if RT_FRAME_NT
+typedef NTf<int> FInt;
+typedef NTf<float> FFloat;
+typedef NTV3 FV3;
+typedef NTC3 FC3;
+#else
+typedef int FInt;
+typedef float FFloat;
+typedef V3 FV3;
+typedef C3 FC3;
+#endif
+
 template <int MAXF>
 struct Frame {
-    int obj, state, depth, phase, light, sn;
-    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
-    float ei, et;                    // incidence / transmission refraction index
-    V3 P, N, I;                      // hit point, shading normal (flipped for spheres), I = -ray
-    float cosI;
-    C3 dif, mask, acc;               // diffuse, cumulative shadow mask, running colour
-    float Ft;                        // transmission Fresnel F (main.cpp:966)
+    FInt obj, state, depth, phase, light, sn;
+    FInt stack[MAXF];                // medium stack (incident_object_stack), object indices
+    FFloat ei, et;                   // incidence / transmission refraction index
+    FV3 P, N, I;                     // hit point, shading normal (flipped for spheres), I = -ray
+    FFloat cosI;
+    FC3 dif, mask, acc;              // diffuse, cumulative shadow mask, running colour
+    FFloat Ft;                       // transmission Fresnel F (main.cpp:966)
 };
 
 
@@ -637,8 +705,8 @@ __device__ void node_begin(const Params &p, Frame<MAXF> &f, V3 o, V3 d, float t)
     f.I = I;
     f.cosI = cosI;
     f.dif = dif;
-    f.mask = {1.0f, 1.0f, 1.0f};
-    f.acc = {0.0f, 0.0f, 0.0f};      // tmp_specular while lights run
+    f.mask = C3{1.0f, 1.0f, 1.0f};
+    f.acc = C3{0.0f, 0.0f, 0.0f};    // tmp_specular while lights run
     f.light = 0;
     f.phase = PH_LIGHT;
 }
@@ -771,14 +839,10 @@ __device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAX
 }
 
 // Lane state between scans.
-// RT_GLOBAL_FRAMES: the frames live in a device buffer, each lane's MAXF frames
-// contiguous (AoS per lane).  Compiler scratch interleaves lanes per dword, so
-// a store by the ~30 % of lanes active in a shading branch dirties whole
-// sectors of mostly-unchanged neighbours and the write-back traffic is ~4x the
-// bytes written; per-lane contiguous frames only dirty the lane's own sectors.
-#ifndef RT_GLOBAL_FRAMES
-#define RT_GLOBAL_FRAMES 1
-#endif
+// RT_GLOBAL_FRAMES: compiler scratch interleaves lanes per dword, so a store by
+// the ~30 % of lanes active in a shading branch dirties whole sectors of
+// mostly-unchanged neighbours and the write-back traffic is ~4x the bytes
+// written; per-lane contiguous frames only dirty the lane's own sectors.
 template <int MAXF>
 struct LaneState {
 #if RT_GLOBAL_FRAMES
@@ -1023,6 +1087,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
     int px = 0, py = 0;
+#if RT_PROF >= 2
+    cnt.t_fetch = cnt.t_trip = 0;
+#endif
 #if RT_PROF
     cnt.trips = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
@@ -1152,6 +1219,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[28], t_end - t_start);         // sum of wave lifetimes
         atomicAdd(&st[29], 1ull);                    // waves
     }
+#if RT_PROF >= 2
+    atomicAdd(&st[30], cnt.t_fetch);
+    atomicAdd(&st[31], cnt.t_trip);
+#endif
 #endif
 }
 

@@ -65,6 +65,8 @@ def main():
                          "tail": (c[26] - c[25]) / 100.0, "mean_wave_tail": c[27] / max(1, c[29]) / 100.0,
                          "mean_wave_life": c[28] / max(1, c[29]) / 100.0, "waves": c[29]}
                         if c[29] else None),
+        "inner_trip_cycles": ({"fetch": c[30] / max(1, c[6] // 4), "trip": c[31] / max(1, c[6] // 4)}
+                              if c[31] else None),
         "raw": c,
     }
     print(json.dumps(res, indent=1))
