@@ -569,15 +569,29 @@ enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_
 #ifndef RT_GLOBAL_FRAMES
 #define RT_GLOBAL_FRAMES 1
 #endif
+// RT_FRAME_NT: 0 plain accesses; 1 non-temporal loads; 2 relaxed agent-scope
+// atomic loads (global_load ... sc1); 3 non-temporal loads and stores (the
+// stores then stream past L2 as well: 2.2x slower, measured).  Stores are
+// plain for 1 and 2.
 #ifndef RT_FRAME_NT
-#define RT_FRAME_NT RT_GLOBAL_FRAMES
+#define RT_FRAME_NT 0
 #endif
 template <typename T>
 struct NTf {
     T v;
-    __device__ __forceinline__ operator T() const { return __builtin_nontemporal_load(&v); }
+    __device__ __forceinline__ operator T() const {
+#if RT_FRAME_NT == 2
+        return __hip_atomic_load(&v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        return __builtin_nontemporal_load(&v);
+#endif
+    }
     __device__ __forceinline__ NTf &operator=(T x) {
+#if RT_FRAME_NT == 3
         __builtin_nontemporal_store(x, &v);
+#else
+        v = x;
+#endif
         return *this;
     }
     __device__ __forceinline__ NTf &operator=(const NTf &o) { return *this = (T)o; }
