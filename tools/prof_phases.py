@@ -29,10 +29,16 @@ def main():
         i = args.index("--rows")
         rows = tuple(int(v) for v in args[i + 1].split(":"))
         del args[i:i + 2]
+    kw = {}                           # --objects S,T -> override sphere / triangle counts
+    if "--objects" in args:
+        i = args.index("--objects")
+        sp, tr = (int(v) for v in args[i + 1].split(","))
+        kw = dict(n_spheres=sp, n_tris=tr, tag=f"obj{sp}_{tr}")
+        del args[i:i + 2]
     cfg = args[0] if args else "C3"
     opts = dict(a.split("=") for a in args[1:])
     d = tempfile.mkdtemp(prefix="rtprof_")
-    path = gen.write_scene(d, cfg)
+    path = gen.write_scene(d, cfg, **kw)
     hs = rtamd.HostScene(path, cwd=d)
     gs = rtamd.GpuScene(hs)
     for k, v in opts.items():
@@ -52,7 +58,7 @@ def main():
     shade, trace, bf, iters, lanes, wtrips, ltrips = c[9:16]
     tot = shade + trace + bf
     res = {
-        "config": cfg, "rows": rows, "options": opts, "kernel_ms": st.kernel_ms,
+        "config": cfg, "objects": kw, "rows": rows, "options": opts, "kernel_ms": st.kernel_ms,
         "cycles_split": {"shade_refill": shade / tot, "trace": trace / tot, "bf_scan": bf / tot} if tot else None,
         "outer_iterations": iters,
         "trace_lane_occupancy": lanes / (64 * iters) if iters else None,
