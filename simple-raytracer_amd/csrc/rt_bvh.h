@@ -145,6 +145,71 @@ inline void collapse4(const Result &R, Result4 &Q) {
     Q.nodes[0].max_stack = Q.max_stack;
 }
 
+// Quantised 4-wide node (64 B = 4 x 16 B; Ylitie et al. 2017 style): the
+// node's box origin, one power-of-two scale per axis, the children's bounds as
+// 8-bit multiples of it rounded outward, and the links.  Child box on axis a:
+// [origin_a + qlo * 2^e_a, origin_a + qhi * 2^e_a] -- it contains the float
+// box exactly (real arithmetic); the device's slab-test rounding is of the
+// order of ulp(D), far inside the primitives' padding (rt_kernels.hip).
+struct Node4Q {
+    float origin[3];
+    uint8_t exp[4];          // biased (+127) exponents of the x, y, z scales; [3] unused
+    uint32_t qlo[3];         // per axis: child i's lower bound in byte i
+    uint32_t qhi[3];         // per axis: child i's upper bound in byte i
+    int32_t link[4];
+    int32_t pad[2];
+};
+static_assert(sizeof(Node4Q) == 64, "quantised node layout");
+
+// Returns false if a child box is not finite (NaN/inf geometry): the caller
+// then uses the brute-force scan.
+inline bool quantize4(const Result4 &Q, std::vector<Node4Q> &out) {
+    out.assign(Q.nodes.size(), Node4Q{});
+    for (size_t k = 0; k < Q.nodes.size(); k++) {
+        const Node4 &n = Q.nodes[k];
+        Node4Q &z = out[k];
+        for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
+        z.pad[0] = z.pad[1] = 0;
+        z.exp[3] = 0;
+        for (int a = 0; a < 3; a++) {
+            double lo = INFINITY, hi = -INFINITY;
+            auto empty = [&](int i) {              // no slot, or an empty leaf (inverted box)
+                return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]);
+            };
+            for (int i = 0; i < 4; i++) {
+                if (empty(i)) continue;
+                if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
+                lo = std::min(lo, (double)n.lo[a][i]);
+                hi = std::max(hi, (double)n.hi[a][i]);
+            }
+            if (!(lo <= hi)) lo = hi = 0.0;              // no child at all
+            z.origin[a] = (float)lo;                     // exact: lo is a float
+            // smallest scale 2^e with 255 * 2^e >= extent (normal floats only)
+            double ext = hi - lo;
+            int e = -126;
+            while (e < 127 && std::ldexp(255.0, e) < ext) e++;
+            z.exp[a] = (uint8_t)(e + 127);
+            double sc = std::ldexp(1.0, e);
+            uint32_t ql = 0, qh = 0;
+            for (int i = 0; i < 4; i++) {
+                uint32_t l = 255, h = 0;                 // empty slot: inverted box
+                if (!empty(i)) {
+                    // exact in double: float differences, power-of-two scale
+                    double fl = std::floor(((double)n.lo[a][i] - lo) / sc);
+                    double fh = std::ceil(((double)n.hi[a][i] - lo) / sc);
+                    l = (uint32_t)std::max(0.0, std::min(255.0, fl));
+                    h = (uint32_t)std::max(0.0, std::min(255.0, fh));
+                }
+                ql |= l << (8 * i);
+                qh |= h << (8 * i);
+            }
+            z.qlo[a] = ql;
+            z.qhi[a] = qh;
+        }
+    }
+    return true;
+}
+
 // Renumber Q's nodes breadth-first (root stays 0), so that the top levels of
 // the tree are nodes [0, K) for any K: the device keeps that prefix in LDS.
 inline void bfs_order(Result4 &Q) {

@@ -149,7 +149,6 @@ struct Params {
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int bvh_stack;                       // BVH: LDS stack entries per lane (worst case of the tree)
-    int lds_nodes;                       // BVH: nodes [0, lds_nodes) (the top levels, BFS order) served from LDS
     void *__restrict__ frames;           // RT_GLOBAL_FRAMES: grid x kBlock x MAXF ShadeRay frames
 };
 
@@ -307,6 +306,9 @@ enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY 
 #define RT_ORDERED_SHADOW 0
 #endif
 constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
+#ifndef RT_QNODE
+#define RT_QNODE 1                       // 1: 64-B quantised nodes (rt_bvh.h Node4Q), 0: 128-B float nodes
+#endif
 constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
@@ -394,7 +396,7 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 // visited together.  Node visits stay one dependent fetch each, and the leaf
 // code runs with most lanes active instead of in almost every wave trip (+6 %
 // over an if-if loop).  The result does not depend on the visiting order.
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const float4 *lnodes, Counters &cnt) {
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
     const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
@@ -408,16 +410,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
     // One 4-wide node (rt_bvh.h Node4: lo.x/y/z rows, hi.x/y/z rows, links):
     // slab-test the children, push the far hits, continue with the nearest,
     // park the first leaf reached.
-    auto visit = [&](float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz, int4 lk) {
+    // children (entry, exit) distances -> push the far hits, continue with the
+    // nearest, park the first leaf reached
+    auto descend = [&](float n0, float f0, float n1, float f1, float n2, float f2, float n3, float f3, int4 lk) {
 #if RT_PROF
         cnt.trips++;
 #endif
-        float thi = q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
-        float n0, f0, n1, f1, n2, f2, n3, f3;
-        slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, ix, iy, iz, ox, oy, oz, tlo, thi, n0, f0);
-        slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, ix, iy, iz, ox, oy, oz, tlo, thi, n1, f1);
-        slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, ix, iy, iz, ox, oy, oz, tlo, thi, n2, f2);
-        slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, ix, iy, iz, ox, oy, oz, tlo, thi, n3, f3);
         cnt.boxes += 4;
         // entry distance of each hit child, +inf for a miss or an empty slot
         float k0 = ((n0 <= f0) & (lk.x != rtbvh::kEmpty)) ? n0 : kInf;
@@ -455,35 +453,75 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
             node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
         }
     };
+    auto thi_now = [&] {
+        return q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
+    };
+    // full-precision node (rt_bvh.h Node4)
+    auto visit = [&](float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz, int4 lk) {
+        float thi = thi_now();
+        float n0, f0, n1, f1, n2, f2, n3, f3;
+        slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, ix, iy, iz, ox, oy, oz, tlo, thi, n0, f0);
+        slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, ix, iy, iz, ox, oy, oz, tlo, thi, n1, f1);
+        slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, ix, iy, iz, ox, oy, oz, tlo, thi, n2, f2);
+        slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, ix, iy, iz, ox, oy, oz, tlo, thi, n3, f3);
+        descend(n0, f0, n1, f1, n2, f2, n3, f3, lk);
+    };
+    // quantised node (rt_bvh.h Node4Q): plane a of child i at
+    // origin_a + q * 2^e_a, i.e. t = q * (2^e_a / d_a) + (origin_a - o_a) / d_a
+    // = fma(q, A_a, B_a) -- one fma per plane, like the full-precision slab;
+    // the rounding (~ulp(D) in distance) is far inside the primitive padding.
+    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3) {
+        float thi = thi_now();
+        unsigned ex = __float_as_uint(w0.w);
+        // 2^e * (1/d): exact power-of-two scaling, kept finite (1/d can be 1e30)
+        float Ax = clampr(__uint_as_float((ex & 0xffu) << 23) * ix, -kFltMax, kFltMax);
+        float Ay = clampr(__uint_as_float(((ex >> 8) & 0xffu) << 23) * iy, -kFltMax, kFltMax);
+        float Az = clampr(__uint_as_float(((ex >> 16) & 0xffu) << 23) * iz, -kFltMax, kFltMax);
+        float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
+        unsigned qlx = __float_as_uint(w1.x), qly = __float_as_uint(w1.y), qlz = __float_as_uint(w1.z);
+        unsigned qhx = __float_as_uint(w1.w), qhy = __float_as_uint(w2.x), qhz = __float_as_uint(w2.y);
+        int4 lk = make_int4(__float_as_int(w2.z), __float_as_int(w2.w), __float_as_int(w3.x), __float_as_int(w3.y));
+        float tn[4], tf[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int sh = 8 * i;
+            float t0x = fmaf((float)((qlx >> sh) & 0xffu), Ax, Bx), t1x = fmaf((float)((qhx >> sh) & 0xffu), Ax, Bx);
+            float t0y = fmaf((float)((qly >> sh) & 0xffu), Ay, By), t1y = fmaf((float)((qhy >> sh) & 0xffu), Ay, By);
+            float t0z = fmaf((float)((qlz >> sh) & 0xffu), Az, Bz), t1z = fmaf((float)((qhz >> sh) & 0xffu), Az, Bz);
+            tn[i] = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tlo));
+            tf[i] = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
+        }
+        descend(tn[0], tf[0], tn[1], tf[1], tn[2], tf[2], tn[3], tf[3], lk);
+    };
     // The root (every trace starts there; wave-uniform) comes through scalar
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
     // (loads and stores share vmcnt, in order).
+#if RT_QNODE
+    visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3));
+#else
     visit(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4), sld4(p.bvh, 5),
           [&] {
               float4 l = sld4(p.bvh, 6);
               return make_int4(__float_as_int(l.x), __float_as_int(l.y), __float_as_int(l.z), __float_as_int(l.w));
           }());
+#endif
     for (;;) {
         while (node >= 0) {
 #if RT_PROF >= 2
             const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
-            // the top of the tree may come from LDS (lds_nodes), the rest from
-            // global memory; 7 float4 per node either way (address-space-typed
-            // pointers: the two paths must not merge into one flat load)
-            float4 lx, ly, lz, hx, hy, hz, lkf;
-            if (node < p.lds_nodes) {
-                const __attribute__((address_space(3))) f4v *N =
-                    (const __attribute__((address_space(3))) f4v *)(lnodes) + 7 * node;
-                lx = f4(N[0]), ly = f4(N[1]), lz = f4(N[2]), hx = f4(N[3]), hy = f4(N[4]), hz = f4(N[5]);
-                lkf = f4(N[6]);
-            } else {
-                const __attribute__((address_space(1))) f4v *N =
-                    (const __attribute__((address_space(1))) f4v *)(p.bvh) + 8 * node;
-                lx = f4(N[0]), ly = f4(N[1]), lz = f4(N[2]), hx = f4(N[3]), hy = f4(N[4]), hz = f4(N[5]);
-                lkf = f4(N[6]);
-            }
+#if RT_QNODE
+            const float4 *N = p.bvh + 4 * node;
+            float4 w0 = N[0], w1 = N[1], w2 = N[2], w3 = N[3];
+#if RT_PROF >= 2
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w3.x) : "memory");
+            cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
+#endif
+            visit_q(w0, w1, w2, w3);
+#else
+            const float4 *N = p.bvh + 8 * node;
+            float4 lx = N[0], ly = N[1], lz = N[2], hx = N[3], hy = N[4], hz = N[5], lkf = N[6];
             int4 lk = make_int4(__float_as_int(lkf.x), __float_as_int(lkf.y), __float_as_int(lkf.z),
                                 __float_as_int(lkf.w));
 #if RT_PROF >= 2
@@ -491,6 +529,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, const 
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
             visit(lx, ly, lz, hx, hy, hz, lk);
+#endif
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
@@ -1069,16 +1108,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: hits[k * kBlock], k < kHits
     int *stk = hits + kHits * kBlock;                       //           stack[k * kBlock]
-    // MODE_BVH node cache after the stacks: the first lds_nodes nodes, 7 float4
-    // each (a 112-B stride spreads different nodes over the LDS banks)
-    float4 *lnodes = lds + (kHits + p.bvh_stack) * (kBlock / 4);
-    if (MODE == MODE_BVH && p.lds_nodes > 0) {
-        for (int i = threadIdx.x; i < 7 * p.lds_nodes; i += blockDim.x) {
-            int nd = i / 7, k = i - nd * 7;
-            lnodes[i] = p.bvh[8 * nd + k];
-        }
-        __syncthreads();
-    }
     Query q;
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
@@ -1167,7 +1196,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(pending && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (pending && !q.bf) bvh_trace(q, p, stk, hits, lnodes, cnt);
+            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1266,9 +1295,6 @@ struct rt_scene {
     std::vector<float> h_ofac;
     int bvh_depth = 0;
     int bvh_stack = 0;
-    int lds_nodes = 0;                 // BVH nodes cached in LDS per block
-    long long opt_lds_nodes = 0;       // -1 auto (fill the block's LDS share), else that many;
-                                       // off by default: C3 4184 vs 4204 Mrays/s without
     bool bvh_ok = false;
     hipStream_t last_stream = nullptr;
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
@@ -1298,8 +1324,7 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
     if (mode == MODE_BVH)
-        return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int) +
-               (size_t)s->lds_nodes * 7 * sizeof(float4);
+        return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int);
     return 0;
 }
 
@@ -1405,15 +1430,6 @@ int build_bvh(rt_scene *s, double D) {
     s->bvh_depth = Q.depth;
     s->bvh_stack = Q.max_stack;
     s->bvh_nodes = (long long)Q.nodes.size();
-    // LDS node cache: what the stacks leave of the block's share of the CU's
-    // 160 KB at RT_MIN_WAVES blocks per CU
-    {
-        long long budget = (163840 / RT_MIN_WAVES) & ~1023LL;
-        long long used = (long long)(kHits + std::max(1, s->bvh_stack)) * kBlock * (long long)sizeof(int);
-        long long k = std::max(0LL, (budget - used) / (7 * (long long)sizeof(float4)));
-        if (s->opt_lds_nodes >= 0) k = s->opt_lds_nodes;
-        s->lds_nodes = (int)std::min<long long>(k, s->bvh_nodes);
-    }
     // leaf records: face = its 5 scan words with (key, shadow factor) in the
     // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
     std::vector<float4> rec;
@@ -1434,6 +1450,15 @@ int build_bvh(rt_scene *s, double D) {
             return 2;
         });
     rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
+#if RT_QNODE
+    std::vector<rtbvh::Node4Q> QQ;
+    if (ok && !Q.nodes.empty() && !rtbvh::quantize4(Q, QQ)) ok = false;   // non-finite geometry: scan
+    const void *nodes = QQ.data();
+    size_t node_bytes = QQ.size() * sizeof(rtbvh::Node4Q);
+#else
+    const void *nodes = Q.nodes.data();
+    size_t node_bytes = Q.nodes.size() * sizeof(rtbvh::Node4);
+#endif
     // the device stack holds kStack entries: a deeper tree uses the scan
     s->bvh_ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
     s->bvh_D = D;
@@ -1442,9 +1467,9 @@ int build_bvh(rt_scene *s, double D) {
     if (s->d_leafrec) (void)hipFree(s->d_leafrec);
     s->d_bvh = nullptr;
     s->d_leafrec = nullptr;
-    if (hipMalloc(&s->d_bvh, Q.nodes.size() * sizeof(rtbvh::Node4)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&s->d_bvh, node_bytes) != hipSuccess) return RT_E_NOMEM;
     if (hipMalloc(&s->d_leafrec, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMemcpy(s->d_bvh, Q.nodes.data(), Q.nodes.size() * sizeof(rtbvh::Node4), hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(s->d_bvh, nodes, node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
         (!rec.empty() &&
          hipMemcpy(s->d_leafrec, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess))
         return RT_E_HIP;
@@ -1470,7 +1495,6 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
             p.bvh = s->base.bvh;
             p.leafrec = s->base.leafrec;
             p.bvh_stack = std::max(1, s->bvh_stack);
-            p.lds_nodes = s->lds_nodes;
         }
     }
     if (mode == MODE_SCAN) {
@@ -1693,7 +1717,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
-    else if (k == "lds_nodes") s->opt_lds_nodes = value < 0 ? -1 : value, s->bvh_D = -1.0;
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);

@@ -2,6 +2,7 @@
 // Reads "n seed mode" from argv, builds over random boxes, verifies:
 //   keys are a permutation; links in range; leaf counts <= 15; every stored
 //   child box contains everything below it; depth <= kMaxDepth.
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -130,6 +131,26 @@ int main(int argc, char **argv) {
     }
     if (cov4 != n) { printf("FAIL covered4 %d of %d\n", cov4, n); return 1; }
     if (maxstack > Q.max_stack || Q.nodes[0].max_stack != Q.max_stack) { printf("FAIL max_stack\n"); return 1; }
+    // quantised nodes contain the float child boxes exactly (real arithmetic)
+    {
+        std::vector<Node4Q> QQ;
+        if (!quantize4(Q, QQ)) { printf("FAIL quantize4\n"); return 1; }
+        for (size_t k = 0; k < Q.nodes.size(); k++)
+            for (int a = 0; a < 3; a++) {
+                double sc = std::ldexp(1.0, (int)QQ[k].exp[a] - 127), o = QQ[k].origin[a];
+                for (int i = 0; i < 4; i++) {
+                    unsigned l = (QQ[k].qlo[a] >> (8 * i)) & 255, h = (QQ[k].qhi[a] >> (8 * i)) & 255;
+                    if (Q.nodes[k].link[i] == kEmpty || !(Q.nodes[k].lo[a][i] <= Q.nodes[k].hi[a][i])) {
+                        if (!(l > h)) { printf("FAIL quantize4 empty slot\n"); return 1; }
+                        continue;
+                    }
+                    if (!(o + l * sc <= Q.nodes[k].lo[a][i]) || !(o + h * sc >= Q.nodes[k].hi[a][i])) {
+                        printf("FAIL quantize4 containment\n");
+                        return 1;
+                    }
+                }
+            }
+    }
     // leaf record stream: same keys per leaf, faces first, contiguous words
     {
         Result4 Q2 = Q;
