@@ -68,28 +68,36 @@ struct Result {
 
 inline int32_t leaf_link(int first, int count) { return -(1 + ((first << 4) | count)); }
 
-// 4-wide node (128 B): the children's boxes as SoA rows + links.  Unused
-// slots carry link kEmpty.  Built by collapsing the binary tree (each node
-// absorbs grandchildren, largest surface area first).
+// W-wide node (W = 4: 128 B, W = 8: 240 B; host-side form): the children's
+// boxes as SoA rows + links.  Unused slots carry link kEmpty.  Built by
+// collapsing the binary tree (each node absorbs grandchildren, largest surface
+// area first).
 constexpr int32_t kEmpty = INT32_MIN;
-struct Node4 {
-    float lo[3][4];
-    float hi[3][4];
-    int32_t link[4];
+template <int W>
+struct NodeW {
+    float lo[3][W];
+    float hi[3][W];
+    int32_t link[W];
     int32_t max_stack;       // worst-case traversal stack entries below (root only)
     int32_t pad[3];
 };
+using Node4 = NodeW<4>;
+using Node8 = NodeW<8>;
 static_assert(sizeof(Node4) == 128, "node4 layout");
 
-struct Result4 {
-    std::vector<Node4> nodes;
+template <int W>
+struct ResultW {
+    std::vector<NodeW<W>> nodes;
     int depth = 0;
     int max_stack = 0;       // worst-case entries a near-first traversal pushes
 };
+using Result4 = ResultW<4>;
+using Result8 = ResultW<8>;
 
-// Collapse a binary tree (Result) into 4-wide nodes.
-inline void collapse4(const Result &R, Result4 &Q) {
-    Q = Result4();
+// Collapse a binary tree (Result) into W-wide nodes.
+template <int W>
+inline void collapse(const Result &R, ResultW<W> &Q) {
+    Q = ResultW<W>();
     if (R.nodes.empty()) return;
     struct Child {
         int32_t link;
@@ -104,13 +112,13 @@ inline void collapse4(const Result &R, Result4 &Q) {
         out[1].box.lo[0] = n.r_lo01[0], out[1].box.lo[1] = n.r_lo01[1], out[1].box.lo[2] = n.r_lo2;
         for (int k = 0; k < 3; k++) out[1].box.hi[k] = n.r_hi[k];
     };
-    // returns the node4 index; `stack_in` = entries already on the stack on entry
+    // returns the node index; `stack_in` = entries already on the stack on entry
     std::function<int(int, int, int)> conv = [&](int ni, int depth, int stack_in) -> int {
-        Child ch[4];
+        Child ch[W];
         int n = 2;
         children2(ni, ch);
         for (;;) {
-            if (n == 4) break;
+            if (n == W) break;
             int best = -1;
             float ba = -1;
             for (int i = 0; i < n; i++)
@@ -127,10 +135,11 @@ inline void collapse4(const Result &R, Result4 &Q) {
         // near-first traversal: visiting a child keeps up to (hits - 1) siblings on the stack
         int below = stack_in + (n - 1);
         Q.max_stack = std::max(Q.max_stack, below);
-        int32_t links[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+        int32_t links[W];
+        for (int i = 0; i < W; i++) links[i] = kEmpty;
         for (int i = 0; i < n; i++) links[i] = ch[i].link >= 0 ? conv(ch[i].link, depth + 1, below) : ch[i].link;
-        Node4 &q = Q.nodes[qi];
-        for (int i = 0; i < 4; i++) {
+        NodeW<W> &q = Q.nodes[qi];
+        for (int i = 0; i < W; i++) {
             for (int k = 0; k < 3; k++) {
                 q.lo[k][i] = i < n ? ch[i].box.lo[k] : INFINITY;
                 q.hi[k][i] = i < n ? ch[i].box.hi[k] : -INFINITY;
@@ -144,39 +153,50 @@ inline void collapse4(const Result &R, Result4 &Q) {
     conv(0, 1, 0);
     Q.nodes[0].max_stack = Q.max_stack;
 }
+inline void collapse4(const Result &R, Result4 &Q) { collapse<4>(R, Q); }
 
-// Quantised 4-wide node (64 B = 4 x 16 B; Ylitie et al. 2017 style): the
-// node's box origin, one power-of-two scale per axis, the children's bounds as
-// 8-bit multiples of it rounded outward, and the links.  Child box on axis a:
-// [origin_a + qlo * 2^e_a, origin_a + qhi * 2^e_a] -- it contains the float
-// box exactly (real arithmetic); the device's slab-test rounding is of the
-// order of ulp(D), far inside the primitives' padding (rt_kernels.hip).
-struct Node4Q {
+// Quantised W-wide node (device form; Ylitie et al. 2017 style): the node's
+// box origin, one power-of-two scale per axis, the children's bounds as 8-bit
+// multiples of it rounded outward (child i in byte i % 4 of word i / 4), and
+// the links.  Child box on axis a: [origin_a + qlo * 2^e_a, origin_a + qhi *
+// 2^e_a] -- it contains the float box exactly (real arithmetic); the device's
+// slab-test rounding is of the order of ulp(D), far inside the primitives'
+// padding (rt_kernels.hip).  W = 4: 64 B (4 x 16 B), W = 8: 96 B (6 x 16 B).
+template <int W>
+struct NodeQBody {
     float origin[3];
     uint8_t exp[4];          // biased (+127) exponents of the x, y, z scales; [3] unused
-    uint32_t qlo[3];         // per axis: child i's lower bound in byte i
-    uint32_t qhi[3];         // per axis: child i's upper bound in byte i
-    int32_t link[4];
+    uint32_t qlo[3][W / 4];  // per axis: lower bounds
+    uint32_t qhi[3][W / 4];  // per axis: upper bounds
+    int32_t link[W];
+};
+template <int W>
+struct NodeQ : NodeQBody<W> {
     int32_t pad[2];
 };
-static_assert(sizeof(Node4Q) == 64, "quantised node layout");
+template <>
+struct NodeQ<8> : NodeQBody<8> {};
+using Node4Q = NodeQ<4>;
+using Node8Q = NodeQ<8>;
+static_assert(sizeof(Node4Q) == 64, "quantised node4 layout");
+static_assert(sizeof(Node8Q) == 96, "quantised node8 layout");
 
 // Returns false if a child box is not finite (NaN/inf geometry): the caller
 // then uses the brute-force scan.
-inline bool quantize4(const Result4 &Q, std::vector<Node4Q> &out) {
-    out.assign(Q.nodes.size(), Node4Q{});
+template <int W>
+inline bool quantize(const ResultW<W> &Q, std::vector<NodeQ<W>> &out) {
+    out.assign(Q.nodes.size(), NodeQ<W>{});
     for (size_t k = 0; k < Q.nodes.size(); k++) {
-        const Node4 &n = Q.nodes[k];
-        Node4Q &z = out[k];
-        for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
-        z.pad[0] = z.pad[1] = 0;
+        const NodeW<W> &n = Q.nodes[k];
+        NodeQ<W> &z = out[k];
+        for (int i = 0; i < W; i++) z.link[i] = n.link[i];
         z.exp[3] = 0;
         for (int a = 0; a < 3; a++) {
-            double lo = INFINITY, hi = -INFINITY;
             auto empty = [&](int i) {              // no slot, or an empty leaf (inverted box)
                 return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]);
             };
-            for (int i = 0; i < 4; i++) {
+            double lo = INFINITY, hi = -INFINITY;
+            for (int i = 0; i < W; i++) {
                 if (empty(i)) continue;
                 if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
                 lo = std::min(lo, (double)n.lo[a][i]);
@@ -190,8 +210,8 @@ inline bool quantize4(const Result4 &Q, std::vector<Node4Q> &out) {
             while (e < 127 && std::ldexp(255.0, e) < ext) e++;
             z.exp[a] = (uint8_t)(e + 127);
             double sc = std::ldexp(1.0, e);
-            uint32_t ql = 0, qh = 0;
-            for (int i = 0; i < 4; i++) {
+            for (int w = 0; w < W / 4; w++) z.qlo[a][w] = z.qhi[a][w] = 0;
+            for (int i = 0; i < W; i++) {
                 uint32_t l = 255, h = 0;                 // empty slot: inverted box
                 if (!empty(i)) {
                     // exact in double: float differences, power-of-two scale
@@ -200,27 +220,27 @@ inline bool quantize4(const Result4 &Q, std::vector<Node4Q> &out) {
                     l = (uint32_t)std::max(0.0, std::min(255.0, fl));
                     h = (uint32_t)std::max(0.0, std::min(255.0, fh));
                 }
-                ql |= l << (8 * i);
-                qh |= h << (8 * i);
+                z.qlo[a][i / 4] |= l << (8 * (i % 4));
+                z.qhi[a][i / 4] |= h << (8 * (i % 4));
             }
-            z.qlo[a] = ql;
-            z.qhi[a] = qh;
         }
     }
     return true;
 }
+inline bool quantize4(const Result4 &Q, std::vector<Node4Q> &out) { return quantize<4>(Q, out); }
 
 // Renumber Q's nodes breadth-first (root stays 0), so that the top levels of
-// the tree are nodes [0, K) for any K: the device keeps that prefix in LDS.
-inline void bfs_order(Result4 &Q) {
+// the tree are nodes [0, K) for any K.
+template <int W>
+inline void bfs_order(ResultW<W> &Q) {
     if (Q.nodes.empty()) return;
     std::vector<int32_t> order;          // new -> old
     std::vector<int32_t> remap(Q.nodes.size(), -1);
     order.push_back(0);
     remap[0] = 0;
     for (size_t h = 0; h < order.size(); h++) {
-        const Node4 &n = Q.nodes[order[h]];
-        for (int i = 0; i < 4; i++) {
+        const NodeW<W> &n = Q.nodes[order[h]];
+        for (int i = 0; i < W; i++) {
             int32_t l = n.link[i];
             if (l >= 0 && remap[l] < 0) {
                 remap[l] = (int32_t)order.size();
@@ -228,10 +248,10 @@ inline void bfs_order(Result4 &Q) {
             }
         }
     }
-    std::vector<Node4> out(order.size());
+    std::vector<NodeW<W>> out(order.size());
     for (size_t k = 0; k < order.size(); k++) {
         out[k] = Q.nodes[order[k]];
-        for (int i = 0; i < 4; i++)
+        for (int i = 0; i < W; i++)
             if (out[k].link[i] >= 0) out[k].link[i] = remap[out[k].link[i]];
     }
     Q.nodes.swap(out);
@@ -251,11 +271,11 @@ inline void leaf_decode(int32_t link, int &off, int &nfaces, int &count) {
     nfaces = (v >> 4) & 15;
     count = v & 15;
 }
-template <class IsFace, class Emit>
-inline bool leaf_records(Result4 &Q, const std::vector<int32_t> &keys, IsFace is_face, Emit emit) {
+template <int W, class IsFace, class Emit>
+inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace is_face, Emit emit) {
     size_t words = 0;
-    for (Node4 &n : Q.nodes) {
-        for (int i = 0; i < 4; i++) {
+    for (NodeW<W> &n : Q.nodes) {
+        for (int i = 0; i < W; i++) {
             int32_t l = n.link[i];
             if (l >= 0 || l == kEmpty) continue;
             int v = -l - 1, first = v >> 4, count = v & 15;

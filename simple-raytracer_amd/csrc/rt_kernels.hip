@@ -307,8 +307,13 @@ enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY 
 #endif
 constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
 #ifndef RT_QNODE
-#define RT_QNODE 1                       // 1: 64-B quantised nodes (rt_bvh.h Node4Q), 0: 128-B float nodes
+#define RT_QNODE 1                       // 1: quantised nodes (rt_bvh.h NodeQ), 0: 128-B float 4-wide nodes
 #endif
+#ifndef RT_BVH_WIDTH
+#define RT_BVH_WIDTH 8                   // children per node: 4 (64-B nodes) or 8 (96-B nodes)
+#endif
+static_assert(RT_BVH_WIDTH == 4 || (RT_BVH_WIDTH == 8 && RT_QNODE), "8-wide nodes are quantised only");
+constexpr int kNodeF4 = RT_QNODE ? (RT_BVH_WIDTH == 8 ? 6 : 4) : 8;   // float4 per node
 constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
@@ -493,11 +498,76 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         }
         descend(tn[0], tf[0], tn[1], tf[1], tn[2], tf[2], tn[3], tf[3], lk);
     };
+    // quantised 8-wide node (rt_bvh.h Node8Q, 6 x 16 B): the same planes, the
+    // children ordered near-first by the 19-comparator sorting network for 8
+    // keys (entry distance, link pairs, registers only)
+    auto visit_q8 = [&](float4 w0, float4 w1, float4 w2, float4 w3, float4 w4, float4 w5) {
+#if RT_PROF
+        cnt.trips++;
+#endif
+        cnt.boxes += 8;
+        float thi = thi_now();
+        unsigned ex = __float_as_uint(w0.w);
+        float Ax = clampr(__uint_as_float((ex & 0xffu) << 23) * ix, -kFltMax, kFltMax);
+        float Ay = clampr(__uint_as_float(((ex >> 8) & 0xffu) << 23) * iy, -kFltMax, kFltMax);
+        float Az = clampr(__uint_as_float(((ex >> 16) & 0xffu) << 23) * iz, -kFltMax, kFltMax);
+        float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
+        const unsigned qlx[2] = {__float_as_uint(w1.x), __float_as_uint(w1.y)};
+        const unsigned qly[2] = {__float_as_uint(w1.z), __float_as_uint(w1.w)};
+        const unsigned qlz[2] = {__float_as_uint(w2.x), __float_as_uint(w2.y)};
+        const unsigned qhx[2] = {__float_as_uint(w2.z), __float_as_uint(w2.w)};
+        const unsigned qhy[2] = {__float_as_uint(w3.x), __float_as_uint(w3.y)};
+        const unsigned qhz[2] = {__float_as_uint(w3.z), __float_as_uint(w3.w)};
+        int c[8] = {__float_as_int(w4.x), __float_as_int(w4.y), __float_as_int(w4.z), __float_as_int(w4.w),
+                    __float_as_int(w5.x), __float_as_int(w5.y), __float_as_int(w5.z), __float_as_int(w5.w)};
+        float k[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int wd = i >> 2, sh = 8 * (i & 3);
+            float t0x = fmaf((float)((qlx[wd] >> sh) & 0xffu), Ax, Bx), t1x = fmaf((float)((qhx[wd] >> sh) & 0xffu), Ax, Bx);
+            float t0y = fmaf((float)((qly[wd] >> sh) & 0xffu), Ay, By), t1y = fmaf((float)((qhy[wd] >> sh) & 0xffu), Ay, By);
+            float t0z = fmaf((float)((qlz[wd] >> sh) & 0xffu), Az, Bz), t1z = fmaf((float)((qhz[wd] >> sh) & 0xffu), Az, Bz);
+            float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tlo));
+            float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
+            k[i] = ((tn <= tf) & (c[i] != rtbvh::kEmpty)) ? tn : kInf;
+        }
+#define RT_CSWAP8(a, b)                          \
+    {                                            \
+        bool sw = k[b] < k[a];                   \
+        float tk = sw ? k[b] : k[a];             \
+        k[b] = sw ? k[a] : k[b];                 \
+        k[a] = tk;                               \
+        int tc = sw ? c[b] : c[a];               \
+        c[b] = sw ? c[a] : c[b];                 \
+        c[a] = tc;                               \
+    }
+        RT_CSWAP8(0, 2) RT_CSWAP8(1, 3) RT_CSWAP8(4, 6) RT_CSWAP8(5, 7)
+        RT_CSWAP8(0, 4) RT_CSWAP8(1, 5) RT_CSWAP8(2, 6) RT_CSWAP8(3, 7)
+        RT_CSWAP8(0, 1) RT_CSWAP8(2, 3) RT_CSWAP8(4, 5) RT_CSWAP8(6, 7)
+        RT_CSWAP8(2, 4) RT_CSWAP8(3, 5)
+        RT_CSWAP8(1, 4) RT_CSWAP8(3, 6)
+        RT_CSWAP8(1, 2) RT_CSWAP8(3, 4) RT_CSWAP8(5, 6)
+#undef RT_CSWAP8
+#pragma unroll
+        for (int i = 7; i >= 1; i--)
+            if (k[i] < kInf) stk[(sp++) * kBlock] = c[i];
+        if (k[0] < kInf) {
+            node = c[0];
+        } else {
+            node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+        }
+        if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
+            leaf = node;                       // park it, keep descending
+            node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+        }
+    };
     // The root (every trace starts there; wave-uniform) comes through scalar
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
     // (loads and stores share vmcnt, in order).
-#if RT_QNODE
+#if RT_QNODE && RT_BVH_WIDTH == 8
+    visit_q8(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4), sld4(p.bvh, 5));
+#elif RT_QNODE
     visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3));
 #else
     visit(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4), sld4(p.bvh, 5),
@@ -512,13 +582,20 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
 #if RT_QNODE
-            const float4 *N = p.bvh + 4 * node;
+            const float4 *N = p.bvh + kNodeF4 * node;
             float4 w0 = N[0], w1 = N[1], w2 = N[2], w3 = N[3];
+#if RT_BVH_WIDTH == 8
+            float4 w4 = N[4], w5 = N[5];
+#endif
 #if RT_PROF >= 2
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w3.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
+#if RT_BVH_WIDTH == 8
+            visit_q8(w0, w1, w2, w3, w4, w5);
+#else
             visit_q(w0, w1, w2, w3);
+#endif
 #else
             const float4 *N = p.bvh + 8 * node;
             float4 lx = N[0], ly = N[1], lz = N[2], hx = N[3], hy = N[4], hz = N[5], lkf = N[6];
@@ -1422,10 +1499,10 @@ int build_bvh(rt_scene *s, double D) {
     B.max_leaf = (int)s->opt_bvh_leaf;
     B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
     bool ok = B.build(R);
-    rtbvh::Result4 Q;
+    rtbvh::ResultW<RT_BVH_WIDTH> Q;
     if (ok && !R.nodes.empty()) {
-        rtbvh::collapse4(R, Q);
-        rtbvh::bfs_order(Q);                 // top levels first: the LDS node cache is a prefix
+        rtbvh::collapse<RT_BVH_WIDTH>(R, Q);
+        rtbvh::bfs_order(Q);                 // top levels first (cache locality of the hot nodes)
     }
     s->bvh_depth = Q.depth;
     s->bvh_stack = Q.max_stack;
@@ -1451,10 +1528,10 @@ int build_bvh(rt_scene *s, double D) {
         });
     rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
 #if RT_QNODE
-    std::vector<rtbvh::Node4Q> QQ;
-    if (ok && !Q.nodes.empty() && !rtbvh::quantize4(Q, QQ)) ok = false;   // non-finite geometry: scan
+    std::vector<rtbvh::NodeQ<RT_BVH_WIDTH>> QQ;
+    if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ)) ok = false;     // non-finite geometry: scan
     const void *nodes = QQ.data();
-    size_t node_bytes = QQ.size() * sizeof(rtbvh::Node4Q);
+    size_t node_bytes = QQ.size() * sizeof(QQ[0]);
 #else
     const void *nodes = Q.nodes.data();
     size_t node_bytes = Q.nodes.size() * sizeof(rtbvh::Node4);

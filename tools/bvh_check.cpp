@@ -18,6 +18,126 @@ static bool contains(const float lo[3], const float hi[3], const Box &b) {
     return true;
 }
 
+template <int W>
+static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int &nodes, int &depth, int &stack) {
+    const float inf = INFINITY;
+    // 4-wide collapse: same leaves, contained boxes, every slot valid or empty
+    ResultW<W> Q;
+    collapse<W>(R, Q);
+    size_t n4 = Q.nodes.size();
+    bfs_order(Q);
+    {   // breadth-first: same node count, depth non-decreasing with the index
+        if (Q.nodes.size() != n4) { printf("FAIL bfs size\n"); return 1; }
+        std::vector<int> dep(n4, -1);
+        dep[0] = 0;
+        for (size_t k = 0; k < n4; k++) {
+            if (dep[k] < 0) { printf("FAIL bfs unreachable\n"); return 1; }
+            if (k > 0 && dep[k] < dep[k - 1]) { printf("FAIL bfs order\n"); return 1; }
+            for (int i = 0; i < W; i++) {
+                int32_t l = Q.nodes[k].link[i];
+                if (l >= 0) {
+                    if (l <= (int32_t)k || dep[l] >= 0) { printf("FAIL bfs link\n"); return 1; }
+                    dep[l] = dep[k] + 1;
+                }
+            }
+        }
+    }
+    struct It4 { int link; float lo[3], hi[3]; int stack; };
+    std::vector<It4> s4;
+    s4.push_back({0, {-inf, -inf, -inf}, {inf, inf, inf}, 0});
+    int cov4 = 0, maxstack = 0;
+    while (!s4.empty()) {
+        It4 it = s4.back();
+        s4.pop_back();
+        if (it.link >= 0) {
+            if (it.link >= (int)Q.nodes.size()) { printf("FAIL node4 range\n"); return 1; }
+            const NodeW<W> &nd = Q.nodes[it.link];
+            int nch = 0;
+            for (int i = 0; i < W; i++) nch += nd.link[i] != kEmpty;
+            if (nch < 1) { printf("FAIL empty node4\n"); return 1; }
+            for (int i = 0; i < W; i++) {
+                if (nd.link[i] == kEmpty) continue;
+                It4 c{nd.link[i], {}, {}, it.stack + nch - 1};
+                maxstack = std::max(maxstack, c.stack);
+                for (int k = 0; k < 3; k++) c.lo[k] = nd.lo[k][i], c.hi[k] = nd.hi[k][i];
+                Box cb;
+                for (int k = 0; k < 3; k++) cb.lo[k] = c.lo[k], cb.hi[k] = c.hi[k];
+                if (!contains(it.lo, it.hi, cb) && it.link != 0) { printf("FAIL node4 containment\n"); return 1; }
+                s4.push_back(c);
+            }
+        } else {
+            int v = -it.link - 1, first = v >> 4, count = v & 15;
+            cov4 += count;
+            for (int q = first; q < first + count; q++)
+                if (!contains(it.lo, it.hi, orig[R.keys[q]].box)) { printf("FAIL leaf4 containment\n"); return 1; }
+        }
+    }
+    if (cov4 != n) { printf("FAIL covered4 %d of %d\n", cov4, n); return 1; }
+    if (maxstack > Q.max_stack || Q.nodes[0].max_stack != Q.max_stack) { printf("FAIL max_stack\n"); return 1; }
+    // quantised nodes contain the float child boxes exactly (real arithmetic)
+    {
+        std::vector<NodeQ<W>> QQ;
+        if (!quantize<W>(Q, QQ)) { printf("FAIL quantize4\n"); return 1; }
+        for (size_t k = 0; k < Q.nodes.size(); k++)
+            for (int a = 0; a < 3; a++) {
+                double sc = std::ldexp(1.0, (int)QQ[k].exp[a] - 127), o = QQ[k].origin[a];
+                for (int i = 0; i < W; i++) {
+                    unsigned l = (QQ[k].qlo[a][i / 4] >> (8 * (i % 4))) & 255, h = (QQ[k].qhi[a][i / 4] >> (8 * (i % 4))) & 255;
+                    if (Q.nodes[k].link[i] == kEmpty || !(Q.nodes[k].lo[a][i] <= Q.nodes[k].hi[a][i])) {
+                        if (!(l > h)) { printf("FAIL quantize4 empty slot\n"); return 1; }
+                        continue;
+                    }
+                    if (!(o + l * sc <= Q.nodes[k].lo[a][i]) || !(o + h * sc >= Q.nodes[k].hi[a][i])) {
+                        printf("FAIL quantize4 containment\n");
+                        return 1;
+                    }
+                }
+            }
+    }
+    // leaf record stream: same keys per leaf, faces first, contiguous words
+    {
+        ResultW<W> Q2 = Q;
+        std::vector<int> words;   // one int per 16-B word: the key of its primitive
+        auto is_face = [](int32_t k) { return k % 3 == 0; };
+        bool ok = leaf_records(Q2, R.keys, is_face, [&](int32_t k) {
+            int w = is_face(k) ? 5 : 2;
+            for (int j = 0; j < w; j++) words.push_back(k);
+            return w;
+        });
+        if (!ok) { printf("FAIL leaf_records\n"); return 1; }
+        int seen = 0;
+        for (size_t ni = 0; ni < Q.nodes.size(); ni++)
+            for (int i = 0; i < W; i++) {
+                int32_t a = Q.nodes[ni].link[i], b = Q2.nodes[ni].link[i];
+                if (a >= 0 || a == kEmpty) {
+                    if (a != b) { printf("FAIL leaf_records inner link\n"); return 1; }
+                    continue;
+                }
+                int v = -a - 1, first = v >> 4, count = v & 15;
+                int off, nfc, cnt;
+                leaf_decode(b, off, nfc, cnt);
+                if (cnt != count) { printf("FAIL leaf_records count\n"); return 1; }
+                std::vector<int> want(R.keys.begin() + first, R.keys.begin() + first + count), got;
+                int w = off;
+                for (int q = 0; q < cnt; q++) {
+                    int k = words.at(w);
+                    if ((q < nfc) != is_face(k)) { printf("FAIL leaf_records order\n"); return 1; }
+                    got.push_back(k);
+                    w += is_face(k) ? 5 : 2;
+                }
+                std::sort(want.begin(), want.end());
+                std::sort(got.begin(), got.end());
+                if (want != got) { printf("FAIL leaf_records keys\n"); return 1; }
+                seen += cnt;
+            }
+        if (seen != n) { printf("FAIL leaf_records coverage\n"); return 1; }
+    }
+    nodes = (int)Q.nodes.size();
+    depth = Q.depth;
+    stack = Q.max_stack;
+    return 0;
+}
+
 int main(int argc, char **argv) {
     int n = argc > 1 ? atoi(argv[1]) : 1000;
     int seed = argc > 2 ? atoi(argv[2]) : 1;
@@ -78,118 +198,10 @@ int main(int argc, char **argv) {
     }
     if (covered != n) { printf("FAIL covered %d of %d\n", covered, n); return 1; }
     (void)r;
-    // 4-wide collapse: same leaves, contained boxes, every slot valid or empty
-    Result4 Q;
-    collapse4(R, Q);
-    size_t n4 = Q.nodes.size();
-    bfs_order(Q);
-    {   // breadth-first: same node count, depth non-decreasing with the index
-        if (Q.nodes.size() != n4) { printf("FAIL bfs size\n"); return 1; }
-        std::vector<int> dep(n4, -1);
-        dep[0] = 0;
-        for (size_t k = 0; k < n4; k++) {
-            if (dep[k] < 0) { printf("FAIL bfs unreachable\n"); return 1; }
-            if (k > 0 && dep[k] < dep[k - 1]) { printf("FAIL bfs order\n"); return 1; }
-            for (int i = 0; i < 4; i++) {
-                int32_t l = Q.nodes[k].link[i];
-                if (l >= 0) {
-                    if (l <= (int32_t)k || dep[l] >= 0) { printf("FAIL bfs link\n"); return 1; }
-                    dep[l] = dep[k] + 1;
-                }
-            }
-        }
-    }
-    struct It4 { int link; float lo[3], hi[3]; int stack; };
-    std::vector<It4> s4;
-    s4.push_back({0, {-inf, -inf, -inf}, {inf, inf, inf}, 0});
-    int cov4 = 0, maxstack = 0;
-    while (!s4.empty()) {
-        It4 it = s4.back();
-        s4.pop_back();
-        if (it.link >= 0) {
-            if (it.link >= (int)Q.nodes.size()) { printf("FAIL node4 range\n"); return 1; }
-            const Node4 &nd = Q.nodes[it.link];
-            int nch = 0;
-            for (int i = 0; i < 4; i++) nch += nd.link[i] != kEmpty;
-            if (nch < 1) { printf("FAIL empty node4\n"); return 1; }
-            for (int i = 0; i < 4; i++) {
-                if (nd.link[i] == kEmpty) continue;
-                It4 c{nd.link[i], {}, {}, it.stack + nch - 1};
-                maxstack = std::max(maxstack, c.stack);
-                for (int k = 0; k < 3; k++) c.lo[k] = nd.lo[k][i], c.hi[k] = nd.hi[k][i];
-                Box cb;
-                for (int k = 0; k < 3; k++) cb.lo[k] = c.lo[k], cb.hi[k] = c.hi[k];
-                if (!contains(it.lo, it.hi, cb) && it.link != 0) { printf("FAIL node4 containment\n"); return 1; }
-                s4.push_back(c);
-            }
-        } else {
-            int v = -it.link - 1, first = v >> 4, count = v & 15;
-            cov4 += count;
-            for (int q = first; q < first + count; q++)
-                if (!contains(it.lo, it.hi, orig[R.keys[q]].box)) { printf("FAIL leaf4 containment\n"); return 1; }
-        }
-    }
-    if (cov4 != n) { printf("FAIL covered4 %d of %d\n", cov4, n); return 1; }
-    if (maxstack > Q.max_stack || Q.nodes[0].max_stack != Q.max_stack) { printf("FAIL max_stack\n"); return 1; }
-    // quantised nodes contain the float child boxes exactly (real arithmetic)
-    {
-        std::vector<Node4Q> QQ;
-        if (!quantize4(Q, QQ)) { printf("FAIL quantize4\n"); return 1; }
-        for (size_t k = 0; k < Q.nodes.size(); k++)
-            for (int a = 0; a < 3; a++) {
-                double sc = std::ldexp(1.0, (int)QQ[k].exp[a] - 127), o = QQ[k].origin[a];
-                for (int i = 0; i < 4; i++) {
-                    unsigned l = (QQ[k].qlo[a] >> (8 * i)) & 255, h = (QQ[k].qhi[a] >> (8 * i)) & 255;
-                    if (Q.nodes[k].link[i] == kEmpty || !(Q.nodes[k].lo[a][i] <= Q.nodes[k].hi[a][i])) {
-                        if (!(l > h)) { printf("FAIL quantize4 empty slot\n"); return 1; }
-                        continue;
-                    }
-                    if (!(o + l * sc <= Q.nodes[k].lo[a][i]) || !(o + h * sc >= Q.nodes[k].hi[a][i])) {
-                        printf("FAIL quantize4 containment\n");
-                        return 1;
-                    }
-                }
-            }
-    }
-    // leaf record stream: same keys per leaf, faces first, contiguous words
-    {
-        Result4 Q2 = Q;
-        std::vector<int> words;   // one int per 16-B word: the key of its primitive
-        auto is_face = [](int32_t k) { return k % 3 == 0; };
-        bool ok = leaf_records(Q2, R.keys, is_face, [&](int32_t k) {
-            int w = is_face(k) ? 5 : 2;
-            for (int j = 0; j < w; j++) words.push_back(k);
-            return w;
-        });
-        if (!ok) { printf("FAIL leaf_records\n"); return 1; }
-        int seen = 0;
-        for (size_t ni = 0; ni < Q.nodes.size(); ni++)
-            for (int i = 0; i < 4; i++) {
-                int32_t a = Q.nodes[ni].link[i], b = Q2.nodes[ni].link[i];
-                if (a >= 0 || a == kEmpty) {
-                    if (a != b) { printf("FAIL leaf_records inner link\n"); return 1; }
-                    continue;
-                }
-                int v = -a - 1, first = v >> 4, count = v & 15;
-                int off, nfc, cnt;
-                leaf_decode(b, off, nfc, cnt);
-                if (cnt != count) { printf("FAIL leaf_records count\n"); return 1; }
-                std::vector<int> want(R.keys.begin() + first, R.keys.begin() + first + count), got;
-                int w = off;
-                for (int q = 0; q < cnt; q++) {
-                    int k = words.at(w);
-                    if ((q < nfc) != is_face(k)) { printf("FAIL leaf_records order\n"); return 1; }
-                    got.push_back(k);
-                    w += is_face(k) ? 5 : 2;
-                }
-                std::sort(want.begin(), want.end());
-                std::sort(got.begin(), got.end());
-                if (want != got) { printf("FAIL leaf_records keys\n"); return 1; }
-                seen += cnt;
-            }
-        if (seen != n) { printf("FAIL leaf_records coverage\n"); return 1; }
-    }
-    printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d nodes4=%zu depth4=%d stack4=%d\n", n,
-           R.nodes.size(), leaves, R.depth, maxd, Q.nodes.size(), Q.depth, Q.max_stack);
+    int n4, d4, s4, n8, d8, s8;
+    if (check_wide<4>(R, orig, n, n4, d4, s4)) return 1;
+    if (check_wide<8>(R, orig, n, n8, d8, s8)) return 1;
+    printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d nodes4=%d depth4=%d stack4=%d nodes8=%d depth8=%d "
+           "stack8=%d\n", n, R.nodes.size(), leaves, R.depth, maxd, n4, d4, s4, n8, d8, s8);
     return 0;
 }
