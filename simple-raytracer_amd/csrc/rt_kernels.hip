@@ -997,23 +997,54 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         top = 0;
     } else {
         Frame<MAXF> &f = ls.fr[top];
-        if (f.phase == PH_LIGHT) {                   // main.cpp:952-958
-            f.mask = q.mask;
-            const LightK &lt = p.lights[f.light];
+        // The fields the shadow-result path needs, loaded in ONE batch with
+        // the phase (pinned: the compiler would sink them under the branch and
+        // make them a second dependent round trip).  For a shadow result the
+        // query itself still holds the frame's hit point (q.o = P) and object
+        // (q.self), so those are not loaded at all.
+        const int phase = f.phase;
+        int light = f.light;
+        V3 fI = f.I, fN = f.N;
+        C3 fdif = f.dif, facc = f.acc;
+        asm volatile("" ::"v"(phase), "v"(light), "v"(fI.x), "v"(fI.y), "v"(fI.z), "v"(fN.x), "v"(fN.y),
+                     "v"(fN.z), "v"(fdif.r), "v"(fdif.g), "v"(fdif.b), "v"(facc.r), "v"(facc.g), "v"(facc.b));
+        if (phase == PH_LIGHT) {                     // main.cpp:952-958
+            const LightK &lt = p.lights[light];
             // L as light_vectors computed it for the shadow ray just traced:
             // that ray's direction for a point light, the constant -L for a
             // directional one (q.d is not modified by a trace)
             V3 L = lt.w == 0.0f ? V3{lt.L[0], lt.L[1], lt.L[2]} : q.d;
-            const ObjK &ob = p.objs[f.obj];
+            const ObjK &ob = p.objs[q.self];
             // H only feeds the specular power: rsqrt instead of 3 IEEE
             // divisions (<= 2 ulp; vnorm(0) = NaN either way)
-            V3 h = vadd(L, f.I);
+            V3 h = vadd(L, fI);
             V3 H = vmul(h, __builtin_amdgcn_rsqf(vdot(h, h)));
-            C3 dc = cmulf(cmulf(f.dif, ob.kd), max0(vdot(f.N, L)));
-            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(f.N, H)), ob.n));
+            C3 dc = cmulf(cmulf(fdif, ob.kd), max0(vdot(fN, L)));
+            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(fN, H)), ob.n));
             C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
-            f.acc = cadd(f.acc, cmulc(cmulc(lc, f.mask), cadd(dc, sc)));
-            f.light++;
+            facc = cadd(facc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
+            light++;
+            f.mask = q.mask;
+            f.acc = facc;
+            f.light = light;
+            if (light < p.nl) {
+                // next light's shadow ray from the same point: origin, self
+                // and cumulative mask are already in q (main.cpp:885-928)
+                V3 L2, sd;
+                float dl;
+                bool unb;
+                light_vectors(p.lights[light], q.o, L2, sd, dl, unb);
+                q.d = sd;
+                q.tmin = p.eps;
+                q.tmax = dl;
+                q.unb = unb;
+                q.closest = false;
+                q.skipchk = false;
+                q.skipped = false;
+                q.win = -1;
+                ls.top = top;
+                return RK_SHADOW;
+            }
         } else if (f.phase == PH_REFR) {
             const ObjK &ob = p.objs[f.obj];
             if (q.skipped) {
