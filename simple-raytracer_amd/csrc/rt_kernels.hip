@@ -461,6 +461,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     auto thi_now = [&] {
         return q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
     };
+#if !RT_QNODE
     // full-precision node (rt_bvh.h Node4)
     auto visit = [&](float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz, int4 lk) {
         float thi = thi_now();
@@ -471,6 +472,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, ix, iy, iz, ox, oy, oz, tlo, thi, n3, f3);
         descend(n0, f0, n1, f1, n2, f2, n3, f3, lk);
     };
+#elif RT_BVH_WIDTH == 4
     // quantised node (rt_bvh.h Node4Q): plane a of child i at
     // origin_a + q * 2^e_a, i.e. t = q * (2^e_a / d_a) + (origin_a - o_a) / d_a
     // = fma(q, A_a, B_a) -- one fma per plane, like the full-precision slab;
@@ -498,6 +500,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         }
         descend(tn[0], tf[0], tn[1], tf[1], tn[2], tf[2], tn[3], tf[3], lk);
     };
+#else
     // quantised 8-wide node (rt_bvh.h Node8Q, 6 x 16 B): the same planes, the
     // children ordered near-first by the 19-comparator sorting network for 8
     // keys (entry distance, link pairs, registers only)
@@ -561,6 +564,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
         }
     };
+#endif
     // The root (every trace starts there; wave-uniform) comes through scalar
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
