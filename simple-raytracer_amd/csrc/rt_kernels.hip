@@ -313,7 +313,7 @@ constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
 #define RT_BVH_WIDTH 4                   // children per node: 4 (64-B nodes) or 8 (96-B nodes; C3 4045 vs 4596 Mrays/s)
 #endif
 static_assert(RT_BVH_WIDTH == 4 || (RT_BVH_WIDTH == 8 && RT_QNODE), "8-wide nodes are quantised only");
-constexpr int kNodeF4 = RT_QNODE ? (RT_BVH_WIDTH == 8 ? 6 : 4) : 8;   // float4 per node
+[[maybe_unused]] constexpr int kNodeF4 = RT_QNODE ? (RT_BVH_WIDTH == 8 ? 6 : 4) : 8;   // float4 per node
 constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
@@ -417,7 +417,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     // park the first leaf reached.
     // children (entry, exit) distances -> push the far hits, continue with the
     // nearest, park the first leaf reached
-    auto descend = [&](float n0, float f0, float n1, float f1, float n2, float f2, float n3, float f3, int4 lk) {
+    [[maybe_unused]] auto descend = [&](float n0, float f0, float n1, float f1, float n2, float f2, float n3, float f3, int4 lk) {
 #if RT_PROF
         cnt.trips++;
 #endif
