@@ -342,22 +342,14 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
         int nt = 0;
         int key;
         float fac;
-        // one batch of loads per primitive, sized by its kind (the kind is
-        // known from the link before loading): 5 words for a face, 2 for a
-        // sphere -- a divergent load instruction costs about one lane-cycle
-        // of the CU's address path whatever its width, so no wasted loads
+        // one batch of loads for either kind (a sphere reads 3 words past its
+        // record; the stream is padded for the last one)
         const f4v *RV = reinterpret_cast<const f4v *>(R);
-        float4 f0, f1, f2, f3, f4;
-        if (k < nfc) {
-            f4v w0 = RV[0], w1 = RV[1], w2 = RV[2], w3 = RV[3], w4 = RV[4];
-            asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
-            f0 = ::rt::f4(w0), f1 = ::rt::f4(w1), f2 = ::rt::f4(w2), f3 = ::rt::f4(w3), f4 = ::rt::f4(w4);
-        } else {
-            f4v w0 = RV[0], w1 = RV[1];
-            asm volatile("" ::"v"(w0), "v"(w1));
-            f0 = ::rt::f4(w0), f1 = ::rt::f4(w1);
-            f2 = f3 = f4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        }
+        f4v w0 = RV[0], w1 = RV[1], w2 = RV[2], w3 = RV[3], w4 = RV[4];
+        asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
+        float4 f0 = make_float4(w0.x, w0.y, w0.z, w0.w), f1 = make_float4(w1.x, w1.y, w1.z, w1.w);
+        float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
+        float4 f4 = make_float4(w4.x, w4.y, w4.z, w4.w);
         if (k < nfc) {
             R += 5;
             key = __float_as_int(f4.y);
