@@ -309,9 +309,6 @@ constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
 #ifndef RT_QNODE
 #define RT_QNODE 1                       // 1: quantised nodes (rt_bvh.h NodeQ), 0: 128-B float 4-wide nodes
 #endif
-#ifndef RT_DEEP_PRIO
-#define RT_DEEP_PRIO 0                   // >0: s_setprio(2) for waves with a lane at least this deep
-#endif
 #ifndef RT_BVH_WIDTH
 #define RT_BVH_WIDTH 4                   // children per node: 4 (64-B nodes) or 8 (96-B nodes; C3 4045 vs 4596 Mrays/s)
 #endif
@@ -1298,12 +1295,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         }
         if (!pending) q.tmin = kInf;                 // lane sits this scan out
         if (__ballot(pending) == 0ull) break;
-#if RT_DEEP_PRIO
-        // waves carrying deep ShadeRay trees (the launch's critical paths)
-        // get issue priority, so that less of them is left for the tail
-        if (__ballot(pending && ls.top >= RT_DEEP_PRIO)) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(0);
-#endif
+
         w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
         w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
         w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
