@@ -196,7 +196,7 @@ def test_subtree_stealing_bit_identical(name):
             st = gs.last_stats()
             dbg = gs.debug_counters()
             assert dbg[32] == 0, "subtree-steal watchdog fired"
-            if steal == 2 and name == "C3_64x64.txt":      # glass + reflective materials
+            if steal == 2 and name != "test7_s.txt":
                 assert dbg[33] > 0, "no subtree was stolen"
             imgs.append(np.nan_to_num(buf[:n].cpu().numpy(), nan=-9))
             rays.append((st.primary, st.shadow, st.refraction, st.reflection, st.skip_trans, st.ub_back))
