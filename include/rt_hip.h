@@ -168,8 +168,7 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * [20] BVH nodes, [21] BVH depth, [22] BVH worst-case stack, [23] CUs;
  * RT_PROF timeline (100 MHz ticks): [24] first wave start, [25] work counter
  * drained, [26] last wave end, [27] sum of per-wave tails, [28] sum of wave
- * lifetimes, [29] waves; [32] subtree-steal watchdog fallbacks (0 in a correct
- * run), [33] reflection subtrees stolen.  n <= 40. */
+ * lifetimes, [29] waves.  n <= 32. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

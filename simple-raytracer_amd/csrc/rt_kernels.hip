@@ -150,7 +150,6 @@ struct Params {
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int bvh_stack;                       // BVH: LDS stack entries per lane (worst case of the tree)
     void *__restrict__ frames;           // RT_GLOBAL_FRAMES: grid x kBlock x MAXF ShadeRay frames
-    int steal;                           // reflection-subtree stealing: 0 off, 1 once drained, 2 always
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -301,9 +300,7 @@ struct Counters {
     unsigned long long t_fetch, t_trip;         // inner-node trips: cycles to node data, whole trip
 #endif
 };
-enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4,
-               RK_WAIT = 5,        // no ray: waiting for a stolen reflection subtree
-               RK_TASKDONE = 6 };  // no ray: a stolen subtree's colour was delivered
+enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
 #ifndef RT_ORDERED_SHADOW
 #define RT_ORDERED_SHADOW 0
@@ -317,8 +314,7 @@ constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
 #endif
 static_assert(RT_BVH_WIDTH == 4 || (RT_BVH_WIDTH == 8 && RT_QNODE), "8-wide nodes are quantised only");
 [[maybe_unused]] constexpr int kNodeF4 = RT_QNODE ? (RT_BVH_WIDTH == 8 ? 6 : 4) : 8;   // float4 per node
-constexpr int kNStats = 40;                      // device counter slots (rt_scene_debug_counters)
-constexpr int kStealWaitCap = 1 << 16;           // a waiting lane's watchdog (iterations)
+constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
     return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
@@ -745,12 +741,6 @@ struct Frame {
     FFloat cosI;
     FC3 dif, mask, acc;              // diffuse, cumulative shadow mask, running colour
     FFloat Ft;                       // transmission Fresnel F (main.cpp:966)
-    // subtree stealing (render_kernel): rsteal 3 not stealable, 0 the
-    // reflection child may be stolen, 1 stolen (in progress), 2 its colour is
-    // in rres; tsrc (frame 0 only) >= 0: this lane runs a stolen subtree for
-    // frame tsrc of the frame buffer
-    FInt rsteal, tsrc;
-    FC3 rres;
 };
 
 
@@ -836,7 +826,6 @@ __device__ void node_begin(const Params &p, Frame<MAXF> &f, V3 o, V3 d, float t)
     f.acc = C3{0.0f, 0.0f, 0.0f};    // tmp_specular while lights run
     f.light = 0;
     f.phase = PH_LIGHT;
-    f.rsteal = 3;
 }
 
 // Direction of light l's shadow ray and the L vector (main.cpp:885-928).
@@ -979,7 +968,6 @@ struct LaneState {
     Frame<MAXF> fr[MAXF];
 #endif
     int top;                         // -1: primary ray pending
-    int wait;                        // iterations spent waiting for a stolen subtree
 };
 
 // Advance one lane after its scan: consume the result, run ShadeRay logic
@@ -987,23 +975,8 @@ struct LaneState {
 // done (returns false with `color` set).
 // Returns the kind of the TraceRay it set up in q (RK_SHADOW/RK_REFR/RK_REFL),
 // or RK_NONE when the pixel is finished (`color` set).
-// Workgroup-scope hand-off of a stolen subtree's colour (thief and owner are
-// lanes of one wave: same CU, same L1).
 template <int MAXF>
-__device__ __forceinline__ void steal_deliver(const Params &p, int tsrc, C3 c) {
-    Frame<MAXF> &vf = reinterpret_cast<Frame<MAXF> *>(p.frames)[tsrc];
-    vf.rres = c;
-    __hip_atomic_store(reinterpret_cast<int *>(&vf.rsteal), 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-template <int MAXF>
-__device__ __forceinline__ int steal_state(Frame<MAXF> &f) {
-    return __hip_atomic_load(reinterpret_cast<int *>(&f.rsteal), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// resume: a waiting lane re-runs the current frame forward (no trace result
-// to consume).
-template <int MAXF>
-__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color, bool resume) {
+__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
     int top = ls.top;
     // a closest hit opens frame `top` (primary hit, refraction or reflection
@@ -1011,8 +984,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
     // whose lanes open frames for different reasons runs it once
     bool begin = false;
     // ---- consume the scan result ----
-    if (resume) {
-    } else if (top < 0) {                            // primary (main.cpp:729-758)
+    if (top < 0) {                                   // primary (main.cpp:729-758)
         if (q.win < 0) {
             color = bkg;
             return RK_NONE;
@@ -1025,7 +997,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         f.stack[0] = q.win;
         f.state = ENTERING;
         f.depth = p.depth;
-        f.tsrc = -1;
         begin = true;
         top = 0;
     } else {
@@ -1089,11 +1060,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 c.obj = q.win;
                 c.depth = f.depth - 1;
                 f.phase = PH_REFR_CHILD;
-                if (p.steal) {                       // will this node cast a reflection ray? (main.cpp:1106)
-                    float F0r = (ob.eta - 1) / (ob.eta + 1);
-                    float Fr = schlick(F0r * F0r, f.cosI);
-                    f.rsteal = (f.depth > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) ? 0 : 3;
-                }
                 begin = true;
                 top++;
             } else {
@@ -1110,11 +1076,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 f.phase = PH_REFL_CHILD;
                 begin = true;
                 top++;
-            } else if (top == 0 && p.steal && f.tsrc >= 0) {
-                // a stolen reflection ray missed: the subtree's colour is bkg
-                steal_deliver<MAXF>(p, f.tsrc, bkg);
-                ls.top = -1;
-                return RK_TASKDONE;
             } else {
                 // miss: refl = bkg * F_r; finish this node below
                 const ObjK &ob = p.objs[f.obj];
@@ -1181,21 +1142,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         if (f.phase == PH_REFL) {                    // main.cpp:1103-1124
             float F0 = (ob.eta - 1) / (ob.eta + 1);
             float Fr = schlick(F0 * F0, f.cosI);
-            int rs = p.steal ? steal_state(f) : 3;
-            if (rs == 1 && ++ls.wait < kStealWaitCap) {   // another lane is shading this reflection subtree
-                ls.top = top;
-                return RK_WAIT;
-            }
-            if (rs == 1) {                           // watchdog: never hang the GPU -- shade it here
-                f.rsteal = 3;                        // (counted in stats[32]; a correct run shows 0)
-                rs = 3;
-                atomicAdd(&p.stats[32], 1ull);
-            }
-            ls.wait = 0;
-            if (rs == 2) {                           // ... and has delivered its colour
-                f.acc = cadd(f.acc, cmulf(C3(f.rres), Fr));
-                f.phase = PH_REFL_CHILD + 1;
-            } else if (f.depth > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
+            if (f.depth > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
                 V3 R = vsub(vmul(f.N, (float)(2.0 * (double)f.cosI)), f.I);
                 q.o = f.P;
                 q.d = R;
@@ -1209,9 +1156,8 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 q.win = -1;
                 ls.top = top;
                 return RK_REFL;
-            } else {
-                f.phase = PH_REFL_CHILD + 1;
             }
+            f.phase = PH_REFL_CHILD + 1;
         }
         // node complete: ((dka + spec) + trans) + refl already folded into acc
         C3 c = f.acc;
@@ -1222,11 +1168,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         }
         top--;
         Frame<MAXF> &pf = ls.fr[top];
-        if (top == 0 && p.steal && pf.phase == PH_REFL_CHILD && pf.tsrc >= 0) {
-            steal_deliver<MAXF>(p, pf.tsrc, c);      // the stolen subtree's colour, to its owner
-            ls.top = -1;
-            return RK_TASKDONE;
-        }
         const ObjK &pob = p.objs[pf.obj];
         if (pf.phase == PH_REFR_CHILD) {             // main.cpp:1072-1083
             C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)pf.Ft)), (float)(1.0 - (double)pob.opacity));
@@ -1272,7 +1213,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
-    ls.wait = 0;
 #if RT_GLOBAL_FRAMES
     ls.fr = reinterpret_cast<Frame<MAXF> *>(p.frames) + ((size_t)blockIdx.x * kBlock + threadIdx.x) * MAXF;
 #endif
@@ -1284,10 +1224,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
-    bool waiting = false;      // lane waits for a stolen reflection subtree's colour
     int px = 0, py = 0;
-    // per-wave steal table (MODE_BVH): after the stacks
-    int *stbl = reinterpret_cast<int *>(lds) + (kHits + p.bvh_stack) * kBlock + (threadIdx.x & ~63);
 #if RT_PROF >= 2
     cnt.t_fetch = cnt.t_trip = 0;
 #endif
@@ -1305,16 +1242,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         int kind = RK_NONE;
         if (pending) {
             C3 color;
-            kind = advance<MAXF>(p, ls, q, cnt, color, waiting);
-            waiting = kind == RK_WAIT;
-            pending = kind != RK_NONE && kind != RK_TASKDONE;
+            kind = advance<MAXF>(p, ls, q, cnt, color);
+            pending = kind != RK_NONE;
             if (!pending) {
-                if (kind == RK_NONE) {
-                    float *o = p.out + ((size_t)py * p.W + px) * 3;
-                    o[0] = color.r;
-                    o[1] = color.g;
-                    o[2] = color.b;
-                }
+                float *o = p.out + ((size_t)py * p.W + px) * 3;
+                o[0] = color.r;
+                o[1] = color.g;
+                o[2] = color.b;
                 busy = false;
             }
         }
@@ -1359,65 +1293,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 }
             }
         }
-        // Reflection-subtree stealing (MODE_BVH, p.steal): idle lanes take
-        // over the reflection subtree of a frame whose refraction subtree is
-        // still being shaded by its owner (same wave).  The thief copies the
-        // frame, traces its reflection ray and shades the subtree; the owner
-        // combines the delivered colour exactly where it would have combined
-        // its own.  Shortens the launch's critical path -- the
-        // deepest single pixel -- that sets the tail.
-        if (MODE == MODE_BVH && p.steal && (drained || p.steal == 2)) {
-            unsigned long long idle = __ballot(!busy);
-            if (idle) {
-                int vk = -1;                         // lowest stealable frame of a busy lane
-                if (busy) {
-#pragma unroll
-                    for (int k = 0; k < MAXF - 1; k++) {
-                        if (vk < 0 && k < ls.top && ls.fr[k].phase == PH_REFR_CHILD && ls.fr[k].rsteal == 0) vk = k;
-                    }
-                }
-                unsigned long long vict = __ballot(vk >= 0);
-                if (vict) {
-                    unsigned n = min((unsigned)__popcll(idle), (unsigned)__popcll(vict));
-                    const unsigned long long lt = (1ull << lane) - 1ull;
-                    unsigned rv = (unsigned)__popcll(vict & lt), rt = (unsigned)__popcll(idle & lt);
-                    const int gl = (int)(blockIdx.x * kBlock + threadIdx.x);
-                    if (vk >= 0 && rv < n) {
-                        ls.fr[vk].rsteal = 1;
-                        stbl[rv] = gl * MAXF + vk;  // this frame's index in the frame buffer
-                    }
-                    if (lane == 0) atomicAdd(&p.stats[33], (unsigned long long)n);
-                    __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0): the table writes land
-                    __builtin_amdgcn_wave_barrier();
-                    if (!busy && rt < n) {
-                        int src = stbl[rt];
-                        Frame<MAXF> &f0 = ls.fr[0];
-                        f0 = reinterpret_cast<const Frame<MAXF> *>(p.frames)[src];
-                        f0.phase = PH_REFL;          // its reflection ray (main.cpp:1103-1124) is ours
-                        f0.rsteal = 3;
-                        f0.tsrc = src;
-                        V3 fN = f0.N, fI = f0.I;
-                        float cosI = f0.cosI;
-                        q.o = f0.P;
-                        q.d = vsub(vmul(fN, (float)(2.0 * (double)cosI)), fI);
-                        q.tmin = p.eps;
-                        q.tmax = kFltMax;
-                        q.unb = false;
-                        q.self = -1;
-                        q.closest = true;
-                        q.skipchk = false;
-                        q.skipped = false;
-                        q.win = -1;
-                        ls.top = 0;
-                        kind = RK_REFL;
-                        busy = true;
-                        pending = true;
-                        waiting = false;
-                    }
-                }
-            }
-        }
-        if (!pending || waiting) q.tmin = kInf;      // lane sits this scan out
+        if (!pending) q.tmin = kInf;                 // lane sits this scan out
         if (__ballot(pending) == 0ull) break;
 
         w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
@@ -1425,16 +1301,15 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         if (MODE == MODE_BVH) {
-            const bool tracing = pending && !waiting;
-            q.bf = tracing && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+            q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
 #if RT_PROF
             unsigned long long c1 = __builtin_amdgcn_s_memtime();
             pc_shade += c1 - c0;
             pc_iter++;
-            pc_lanes += (unsigned long long)__popcll(__ballot(tracing && !q.bf));
+            pc_lanes += (unsigned long long)__popcll(__ballot(pending && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (tracing && !q.bf) bvh_trace(q, p, stk, hits, cnt);
+            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1442,13 +1317,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             unsigned long long c2 = __builtin_amdgcn_s_memtime();
             pc_trace += c2 - c1;
 #endif
-            bool need = tracing && q.bf;
+            bool need = pending && q.bf;
             if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
 #if RT_PROF
             pc_bf += __builtin_amdgcn_s_memtime() - c2;
 #endif
         } else {
-            scan<SRC_LDS>(q, p, lds_f, lds_s, pending && !waiting, cnt.ftests, cnt.stests);
+            scan<SRC_LDS>(q, p, lds_f, lds_s, pending, cnt.ftests, cnt.stests);
         }
     }
     unsigned long long *st = p.stats;
@@ -1514,7 +1389,6 @@ struct rt_scene {
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
-    long long opt_steal = 1;           // reflection-subtree stealing: 0 off, 1 once drained, 2 always
     long long opt_bvh_leaf = 8;        // SAH max leaf size
     long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
@@ -1563,7 +1437,7 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
     if (mode == MODE_BVH)
-        return (size_t)(kHits + std::max(1, s->bvh_stack) + 1) * kBlock * sizeof(int);   // + steal table
+        return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int);
     return 0;
 }
 
@@ -1734,7 +1608,6 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
             p.bvh = s->base.bvh;
             p.leafrec = s->base.leafrec;
             p.bvh_stack = std::max(1, s->bvh_stack);
-            p.steal = (int)s->opt_steal;
         }
     }
     if (mode == MODE_SCAN) {
@@ -1957,7 +1830,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
-    else if (k == "steal") s->opt_steal = std::max(0LL, std::min(2LL, value));
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);

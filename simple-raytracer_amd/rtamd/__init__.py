@@ -302,8 +302,8 @@ class GpuScene:
 
     def debug_counters(self) -> list[int]:
         """Raw device counters of the last render (rt_scene_debug_counters)."""
-        buf = (C.c_ulonglong * 40)()
-        _check(hip_lib().rt_scene_debug_counters(self._h, buf, 40), "rt_scene_debug_counters")
+        buf = (C.c_ulonglong * 32)()
+        _check(hip_lib().rt_scene_debug_counters(self._h, buf, 32), "rt_scene_debug_counters")
         return list(buf)
 
 

@@ -55,22 +55,16 @@ def test_scene_parity(name, golden):
         assert diff_px <= MAX_BAD_FRAC, diff_px
 
 
-# (accel, steal): brute-force scan; BVH without subtree stealing; BVH where
-# idle lanes steal reflection subtrees from the start (not only in the tail)
-PATHS = [(0, 0), (1, 0), (1, 2)]
-
-
-@pytest.mark.parametrize("path", PATHS, ids=lambda t: "accel%d_steal%d" % t)
+@pytest.mark.parametrize("accel", [0, 1])
 @pytest.mark.parametrize("name", golden_names(lambda v: v["width"] * v["height"] <= 300 * 300))
-def test_scene_parity_forced_path(name, path, golden):
-    """Every search strategy on every small fixture: the brute-force scan and
-    the BVH (with its exact fallbacks, with and without reflection-subtree
-    stealing), each against the oracle, with identical ray counts."""
-    accel, steal = path
-    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel, "steal": steal})
+def test_scene_parity_forced_path(name, accel, golden):
+    """Both search strategies on every small fixture: the brute-force scan
+    (accel=0) and the BVH (accel=1, with its exact fallbacks), each against
+    the oracle, with identical ray counts."""
+    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel})
     ref, cnt = OracleScene(name, cwd=SCENES).render()
     c = compare(img, ref)
-    tag = "accel%d_steal%d" % path
+    tag = "accel%d" % accel
     _summary[f"{name}@{tag}"] = dict(c, tests=dict(box=st.box_tests, face=st.face_tests,
                                                    sphere=st.sphere_tests))
     assert_parity(img, ref, f"{name} {tag}")
@@ -172,37 +166,6 @@ def test_row_blocks_reassemble(world):
         img[image_rows(H, world, r)] = buf[:n].cpu().numpy()
     assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(full, nan=-9))
     assert rays == st.rays()
-
-
-@pytest.mark.parametrize("name", ["C3_64x64.txt", "test7_s.txt", "edge_glass_faces.txt", "edge_nested_nobkgeta.txt"])
-def test_subtree_stealing_bit_identical(name):
-    """Stealing reflection subtrees only changes which lane shades them: the
-    image is bit-identical to the render without stealing and the ray counts
-    are unchanged -- for the whole image and for a multi-GPU row set."""
-    torch = pytest.importorskip("torch")
-    from rtamd.dist import row_set
-    hs = rtamd.HostScene(name, cwd=SCENES)
-    W, H = hs.width, hs.height
-    cam = hs.camera()
-    gs = rtamd.GpuScene(hs)
-    gs.set_option("accel", 1)
-    for world, rank in [(1, 0), (3, 1)]:
-        y0, b, step, n, per = row_set(H, world, rank)
-        imgs, rays = [], []
-        for steal in (0, 1, 2):
-            gs.set_option("steal", steal)
-            buf = torch.full((per, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
-            gs.render_row_blocks_async(cam, W, H, y0, b, step, n, buf.data_ptr())
-            st = gs.last_stats()
-            dbg = gs.debug_counters()
-            assert dbg[32] == 0, "subtree-steal watchdog fired"
-            if steal == 2 and name != "test7_s.txt":
-                assert dbg[33] > 0, "no subtree was stolen"
-            imgs.append(np.nan_to_num(buf[:n].cpu().numpy(), nan=-9))
-            rays.append((st.primary, st.shadow, st.refraction, st.reflection, st.skip_trans, st.ub_back))
-        for i in (1, 2):
-            assert np.array_equal(imgs[0], imgs[i]), (world, rank, i)
-            assert rays[0] == rays[i]
 
 
 def test_render_into_device_memory():

@@ -73,8 +73,6 @@ def main():
                         if c[29] else None),
         "inner_trip_cycles": ({"fetch": c[30] / max(1, c[6] // 4), "trip": c[31] / max(1, c[6] // 4)}
                               if c[31] else None),
-        "steals": c[33] if len(c) > 33 else None,
-        "steal_watchdog": c[32] if len(c) > 32 else None,
         "raw": c,
     }
     print(json.dumps(res, indent=1))
