@@ -52,6 +52,9 @@ def parse_args():
                     help="cpu_baseline: the reference renders the same scene at NxN")
     ap.add_argument("--option", action="append", default=[],
                     help="kernel option key=value (rt_scene_set_option)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: step k renders on stream k mod F (rt_scene option "
+                         "'inflight'), so one frame's tail overlaps the next frame's work")
     ap.add_argument("--out-json", default=None)
     return ap.parse_args()
 
@@ -136,52 +139,60 @@ def main() -> None:
 
     # strong scaling: block-interleaved row sets (rtamd/dist.py), equal-size
     # buffers for the gather
-    from rtamd.dist import alloc_strips, gather_strips, row_set
+    from rtamd.dist import ImageGather, row_set
     ry0, rblock, rstep, nrows, _ = row_set(H, world, rank)
-    strip, gather_list = alloc_strips(H, W, world, rank, "cuda", torch)
-    # a dedicated (non-null) stream: the render kernel, its timing events and
-    # the RCCL gather are all ordered on it
-    stream = torch.cuda.Stream()
+    # F frames in flight: frame k renders into buffer k mod F, ordered on
+    # stream k mod F (the render on a library stream of its own, the gather
+    # after it); frame k+1 on the next stream overlaps frame k's tail.
+    F = max(1, min(4, args.inflight))
+    if F > 1:
+        gs.set_option("inflight", F)
+    gathers = [ImageGather(H, W, world, rank, "cuda", torch) for _ in range(F)]
+    streams = [torch.cuda.Stream() for _ in range(F)]
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        if nrows > 0:
-            gs.render_row_blocks_async(cam, W, H, ry0, rblock, rstep, nrows, strip.data_ptr(),
-                                       stream.cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
-        if world > 1:
-            gather_strips(strip, gather_list, world, rank, H, dist, torch)
+    def step(k):
+        s, g = streams[k % F], gathers[k % F]
+        with torch.cuda.stream(s):
+            if nrows > 0:
+                gs.render_row_blocks_async(cam, W, H, ry0, rblock, rstep, nrows, g.strip.data_ptr(),
+                                           s.cuda_stream)
+            if world > 1:
+                g.gather(dist)
 
-    torch.cuda.set_stream(stream)
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
     torch.cuda.synchronize()
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(events[k])
+        step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in events]
     st = gs.last_stats()          # counters of the last timed render (identical every step)
     my_rays = st.rays()
+    # device time of that launch (first wave start .. last wave end, the
+    # kernel's own clock; what rocprofv3 reports per dispatch)
+    kernel_ms = [st.kernel_ms]
+    # single-frame latency (nothing else in flight), after the timed region
+    torch.cuda.synchronize()
+    lat0 = time.perf_counter()
+    step(0)
+    torch.cuda.synchronize()
+    latency_ms = (time.perf_counter() - lat0) * 1e3
 
-    t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms))], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms)), latency_ms], dtype=torch.float64,
+                     device="cuda")
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, rays_total, kmax = float(tmax[0]), float(tsum[1]), float(tmax[2])
+        elapsed, rays_total, kmax, latency_ms = float(tmax[0]), float(tsum[1]), float(tmax[2]), float(tmax[3])
     else:
         rays_total, kmax = float(my_rays), float(np.mean(kernel_ms))
 
@@ -219,6 +230,7 @@ def main() -> None:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "frame_latency_ms": round(latency_ms, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -227,11 +239,14 @@ def main() -> None:
             "config": {"workload": WORKLOADS[args.config], "imsize": [W, H], "spheres": ns,
                        "triangles": nt, "depth": cfg["depth"], "lights": 2,
                        "rays_per_step": int(rays_total), "parallelism": f"interleaved 8-row blocks x{world}"
-                       + (" + RCCL gather" if world > 1 else "")},
+                       + (" + RCCL gather" if world > 1 else ""), "frames_in_flight": F},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic, "kernel": "render_kernel",
                          "kernel_ms": round(float(np.mean(kernel_ms)), 3),
+                         "per_step": {"achieved": round(flops / (elapsed / args.steps) / 1e12, 3),
+                                      "frac": round(flops / (elapsed / args.steps) / 1e12
+                                                    / PEAK_FP32_TFLOPS, 4)},
                          "rays_per_launch": my_rays,
                          "tests_per_launch": {"box": st.box_tests, "face": st.face_tests,
                                               "sphere": st.sphere_tests},

@@ -143,8 +143,10 @@ int rt_render_rows(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, 
                    rt_stats *stats);
 
 /* Same, asynchronous on `hip_stream` (a hipStream_t, NULL = the scene's own
- * stream); out_rgb must be device memory.  rt_scene_last_stats() waits for
- * the render and returns its counters. */
+ * stream); out_rgb must be device memory.  The render is ordered after the
+ * work already queued on hip_stream and before the work queued after it.
+ * rt_scene_last_stats() waits for the last render and returns its counters
+ * (kernel_ms = first wave start .. last wave end of its launch). */
 int rt_render_rows_async(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
                          void *hip_stream);
 int rt_scene_last_stats(rt_scene *scene, rt_stats *stats);
@@ -158,7 +160,12 @@ int rt_render_row_blocks_async(rt_scene *scene, const rt_camera *cam, int W, int
 
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
- * (persistent blocks, 0 = occupancy), "depth" (recursion depth override). */
+ * (persistent blocks, 0 = occupancy), "depth" (recursion depth override),
+ * "inflight" (1..4, default 1: renders of this scene that may run at once.
+ * With n > 1 each render gets its own work counter, counters and ShadeRay
+ * frame buffer and runs on a library stream, ordered against its caller's
+ * stream by events: renders issued on different caller streams -- independent
+ * frames -- overlap, so one frame's tail is filled by the next frame's work). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
 /* Raw counters of the last render (diagnostics): [0..8] as in rt_stats,
@@ -166,8 +173,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * otherwise), then launch facts: [16] kernel mode (0 scan, 1 LDS scan, 2 BVH),
  * [17] resident blocks per CU, [18] grid, [19] LDS bytes per block,
  * [20] BVH nodes, [21] BVH depth, [22] BVH worst-case stack, [23] CUs;
- * RT_PROF timeline (100 MHz ticks): [24] first wave start, [25] work counter
- * drained, [26] last wave end, [27] sum of per-wave tails, [28] sum of wave
+ * launch timeline (100 MHz ticks): [24] first wave start, [26] last wave end;
+ * RT_PROF builds also [25] work counter drained, [27] sum of per-wave tails, [28] sum of wave
  * lifetimes, [29] waves.  n <= 32. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 

@@ -732,9 +732,12 @@ typedef V3 FV3;
 typedef C3 FC3;
 #endif
 
+// No depth field: frame k of a lane's stack is at recursion depth p.depth - k.
+// At MAXF = 5 (depth 4) a frame is 32 words = one 128-B cache line, and the
+// lane's frames are line-aligned (the buffer is, and 5 x 128 B per lane).
 template <int MAXF>
 struct Frame {
-    FInt obj, state, depth, phase, light, sn;
+    FInt obj, state, phase, light, sn;
     FInt stack[MAXF];                // medium stack (incident_object_stack), object indices
     FFloat ei, et;                   // incidence / transmission refraction index
     FV3 P, N, I;                     // hit point, shading normal (flipped for spheres), I = -ray
@@ -780,6 +783,8 @@ __device__ __forceinline__ float texel(const Params &p, const TexK &t, int x, in
 
 // ShadeRay prologue (main.cpp:785-872): diffuse / texture and the sphere
 // normal flip.  Leaves the frame ready for the light loop.
+static_assert(sizeof(Frame<5>) == 128, "a depth-4 frame is one cache line");
+
 template <int MAXF>
 __device__ void node_begin(const Params &p, Frame<MAXF> &f, V3 o, V3 d, float t) {
     V3 P, N, bary;
@@ -996,7 +1001,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         f.sn = 1;
         f.stack[0] = q.win;
         f.state = ENTERING;
-        f.depth = p.depth;
         begin = true;
         top = 0;
     } else {
@@ -1058,7 +1062,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 Frame<MAXF> &c = ls.fr[top + 1];
                 refr_transition(p, f, c, q.win, cnt);
                 c.obj = q.win;
-                c.depth = f.depth - 1;
                 f.phase = PH_REFR_CHILD;
                 begin = true;
                 top++;
@@ -1072,7 +1075,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 Frame<MAXF> &c = ls.fr[top + 1];
                 refl_transition(p, f, c, q.win);
                 c.obj = q.win;
-                c.depth = f.depth - 1;
                 f.phase = PH_REFL_CHILD;
                 begin = true;
                 top++;
@@ -1119,7 +1121,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             bool tir = (crit < inc) && ((double)inc < kRightAngle);
             float F0 = (f.et - f.ei) / (f.et + f.ei);
             f.Ft = schlick(F0 * F0, f.cosI);
-            if (f.depth > 0 && !tir && (double)ob.opacity < 1.0 && ob.eta > 0) {
+            if (p.depth - top > 0 && !tir && (double)ob.opacity < 1.0 && ob.eta > 0) {
                 float k = sqrtf((float)(1.0 - (double)(snell * snell) * (1.0 - (double)(f.cosI * f.cosI))));
                 V3 T = vadd(vmul(vmul(f.N, -1.0f), k), vmul(vsub(vmul(f.N, f.cosI), f.I), snell));
                 q.o = f.P;
@@ -1142,7 +1144,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         if (f.phase == PH_REFL) {                    // main.cpp:1103-1124
             float F0 = (ob.eta - 1) / (ob.eta + 1);
             float Fr = schlick(F0 * F0, f.cosI);
-            if (f.depth > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
+            if (p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
                 V3 R = vsub(vmul(f.N, (float)(2.0 * (double)f.cosI)), f.I);
                 q.o = f.P;
                 q.d = R;
@@ -1228,11 +1230,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #if RT_PROF >= 2
     cnt.t_fetch = cnt.t_trip = 0;
 #endif
+    // launch timeline on the constant 100 MHz clock (comparable across CUs /
+    // XCDs): first wave start .. last wave end = the launch's device time even
+    // when launches of several frames overlap (rt_scene_last_stats)
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #if RT_PROF
     cnt.trips = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
-    // timeline on the constant 100 MHz clock (comparable across CUs / XCDs)
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_drain = 0;
 #endif
     for (;;) {
@@ -1338,6 +1342,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&st[6], (unsigned long long)cnt.boxes);
     atomicAdd(&st[7], (unsigned long long)cnt.ftests);
     atomicAdd(&st[8], (unsigned long long)cnt.stests);
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        atomicMin(&st[24], t_start);                 // kernel start (first wave)
+        atomicMax(&st[26], t_end);                   // last wave done
+    }
 #if RT_PROF
     if (lane == 0) {
         atomicAdd(&st[9], pc_shade);
@@ -1349,11 +1358,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     }
     atomicAdd(&st[15], (unsigned long long)cnt.trips);
     if (lane == 0) {
-        unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         if (!t_drain) t_drain = t_end;
-        atomicMin(&st[24], t_start);                 // kernel start (first wave)
         atomicMin(&st[25], t_drain);                 // work counter ran out
-        atomicMax(&st[26], t_end);                   // last wave done
         atomicAdd(&st[27], t_end - t_drain);         // sum of per-wave tails
         atomicAdd(&st[28], t_end - t_start);         // sum of wave lifetimes
         atomicAdd(&st[29], 1ull);                    // waves
@@ -1372,18 +1378,33 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 // ===========================================================================
 using namespace rt;
 
-struct rt_scene {
-    int device = 0;
-    hipStream_t stream = nullptr;
+// One render in flight: its work counter, counters, ShadeRay frame buffer and
+// events.  A scene has `inflight` of them (rt_scene_set_option "inflight"):
+// with one, a render runs on the caller's stream; with more, render k runs on
+// slot k mod n's own stream, ordered against the caller's stream by events, so
+// that renders issued on different caller streams (independent frames) overlap:
+// the next frame's workgroups fill the CUs that the current frame's tail leaves
+// idle.
+struct RenderSlot {
+    hipStream_t stream = nullptr;      // slots > 1 only (high priority: its own HW queue pool)
+    hipEvent_t ev_in = nullptr;        // caller stream -> slot stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    Params base{};
-    std::vector<void *> allocs;
-    float *dev_out = nullptr;          // staging buffer when the caller passes host memory
-    size_t dev_out_bytes = 0;
     unsigned int *work = nullptr;
     unsigned long long *stats = nullptr;
     void *d_frames = nullptr;          // RT_GLOBAL_FRAMES buffer
     size_t frames_cap = 0;
+};
+
+struct rt_scene {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Params base{};
+    std::vector<void *> allocs;
+    float *dev_out = nullptr;          // staging buffer when the caller passes host memory
+    size_t dev_out_bytes = 0;
+    std::vector<RenderSlot> slots;     // slots[0] always exists
+    int next_slot = 0;                 // slot of the next render
+    int last_slot = 0;                 // slot of the last render
     int num_cu = 0;
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
@@ -1409,7 +1430,6 @@ struct rt_scene {
     int bvh_depth = 0;
     int bvh_stack = 0;
     bool bvh_ok = false;
-    hipStream_t last_stream = nullptr;
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
     long long bvh_nodes = 0;
     bool last_valid = false;
@@ -1442,7 +1462,7 @@ size_t mode_lds_bytes(const rt_scene *s, int mode) {
 }
 
 template <int MAXF, int MODE>
-hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
+hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_t st) {
     size_t shm = mode_lds_bytes(s, MODE);
     int nb = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE>, kBlock, shm);
@@ -1454,14 +1474,14 @@ hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
     Params pl = p;
 #if RT_GLOBAL_FRAMES
     size_t fbytes = (size_t)grid * kBlock * MAXF * sizeof(Frame<MAXF>);
-    if (s->frames_cap < fbytes) {
-        if (s->d_frames) (void)hipFree(s->d_frames);
-        s->d_frames = nullptr;
-        s->frames_cap = 0;
-        if (hipMalloc(&s->d_frames, fbytes) != hipSuccess) return hipErrorOutOfMemory;
-        s->frames_cap = fbytes;
+    if (slot.frames_cap < fbytes) {
+        if (slot.d_frames) (void)hipFree(slot.d_frames);
+        slot.d_frames = nullptr;
+        slot.frames_cap = 0;
+        if (hipMalloc(&slot.d_frames, fbytes) != hipSuccess) return hipErrorOutOfMemory;
+        slot.frames_cap = fbytes;
     }
-    pl.frames = s->d_frames;
+    pl.frames = slot.d_frames;
 #endif
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
@@ -1472,10 +1492,10 @@ hipError_t launch_one(rt_scene *s, const Params &p, hipStream_t st) {
 }
 
 template <int MAXF>
-hipError_t launch_mode(rt_scene *s, const Params &p, int mode, hipStream_t st) {
-    if (mode == MODE_BVH) return launch_one<MAXF, MODE_BVH>(s, p, st);
-    if (mode == MODE_SCAN_LDS) return launch_one<MAXF, MODE_SCAN_LDS>(s, p, st);
-    return launch_one<MAXF, MODE_SCAN>(s, p, st);
+hipError_t launch_mode(rt_scene *s, RenderSlot &slot, const Params &p, int mode, hipStream_t st) {
+    if (mode == MODE_BVH) return launch_one<MAXF, MODE_BVH>(s, slot, p, st);
+    if (mode == MODE_SCAN_LDS) return launch_one<MAXF, MODE_SCAN_LDS>(s, slot, p, st);
+    return launch_one<MAXF, MODE_SCAN>(s, slot, p, st);
 }
 
 // Distance bound for the BVH padding: from any ray origin (the eye, or a point
@@ -1591,7 +1611,7 @@ int build_bvh(rt_scene *s, double D) {
     return RT_OK;
 }
 
-int launch(rt_scene *s, Params &p, hipStream_t st) {
+int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st) {
     int depth = p.depth < 0 ? 0 : p.depth;
     if (depth > 16) return RT_E_UNSUPPORTED;
     int nobj = p.nf + p.ns;
@@ -1616,10 +1636,55 @@ int launch(rt_scene *s, Params &p, hipStream_t st) {
         if (lds) mode = MODE_SCAN_LDS;
     }
     hipError_t e;
-    if (depth <= 4) e = launch_mode<5>(s, p, mode, st);
-    else if (depth <= 8) e = launch_mode<9>(s, p, mode, st);
-    else e = launch_mode<17>(s, p, mode, st);
+    if (depth <= 4) e = launch_mode<5>(s, slot, p, mode, st);
+    else if (depth <= 8) e = launch_mode<9>(s, slot, p, mode, st);
+    else e = launch_mode<17>(s, slot, p, mode, st);
     return e == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
+void free_slot(RenderSlot &r) {
+    if (r.stream) (void)hipStreamSynchronize(r.stream);
+    if (r.work) (void)hipFree(r.work);
+    if (r.stats) (void)hipFree(r.stats);
+    if (r.d_frames) (void)hipFree(r.d_frames);
+    if (r.ev_in) (void)hipEventDestroy(r.ev_in);
+    if (r.ev0) (void)hipEventDestroy(r.ev0);
+    if (r.ev1) (void)hipEventDestroy(r.ev1);
+    if (r.stream) (void)hipStreamDestroy(r.stream);
+    r = RenderSlot{};
+}
+
+// own_stream: slots of a scene with more than one render in flight get a
+// stream of their own, at the highest priority: HIP keeps a separate hardware
+// queue pool per priority, so the slot's dispatches never queue behind barrier
+// packets of caller (or collective) streams that share a hardware queue.
+int init_slot(RenderSlot &r, bool own_stream) {
+    if (hipMalloc(&r.work, sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&r.stats, kNStats * sizeof(unsigned long long)) != hipSuccess) return RT_E_NOMEM;
+    if (hipEventCreate(&r.ev0) != hipSuccess || hipEventCreate(&r.ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming) != hipSuccess)
+        return RT_E_HIP;
+    if (own_stream) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return RT_E_HIP;
+        if (hipStreamCreateWithPriority(&r.stream, hipStreamNonBlocking, hi) != hipSuccess) return RT_E_HIP;
+    }
+    return RT_OK;
+}
+
+int set_inflight(rt_scene *s, long long n) {
+    if (n < 1 || n > 4) return RT_E_INVALID;
+    if ((size_t)n == s->slots.size()) return RT_OK;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    for (auto &r : s->slots) free_slot(r);
+    s->slots.assign((size_t)n, RenderSlot{});
+    s->next_slot = s->last_slot = 0;
+    s->last_valid = false;
+    for (auto &r : s->slots) {
+        int rc = init_slot(r, n > 1);
+        if (rc) return rc;
+    }
+    return RT_OK;
 }
 
 }  // namespace
@@ -1774,10 +1839,11 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     if (!rc) rc = upload(s, lights, p.lights);
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
-    if (!rc && hipMalloc(&s->work, sizeof(unsigned)) != hipSuccess) rc = RT_E_NOMEM;
-    if (!rc && hipMalloc(&s->stats, kNStats * sizeof(unsigned long long)) != hipSuccess) rc = RT_E_NOMEM;
     if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
-    if (!rc && (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)) rc = RT_E_HIP;
+    if (!rc) {
+        s->slots.assign(1, RenderSlot{});
+        rc = init_slot(s->slots[0], false);
+    }
     if (!rc) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) rc = RT_E_HIP;
@@ -1794,8 +1860,6 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.eta_bkg = desc->eta_bkg;
     p.eps = desc->epsilon;
     p.depth = desc->depth;
-    p.work = s->work;
-    p.stats = s->stats;
     p.dir_bf = 0;
     for (int i = 0; i < desc->n_lights; i++)
         if (desc->lights[i].w == 0.0f && ns > 0) p.dir_bf = 1;
@@ -1809,15 +1873,13 @@ int rt_scene_destroy(rt_scene *s) {
     if (!s) return RT_OK;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (auto &r : s->slots)           // renders still running on caller or slot streams
+        if (r.ev1) (void)hipEventSynchronize(r.ev1);
     for (void *d : s->allocs) (void)hipFree(d);
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_leafrec) (void)hipFree(s->d_leafrec);
     if (s->dev_out) (void)hipFree(s->dev_out);
-    if (s->work) (void)hipFree(s->work);
-    if (s->stats) (void)hipFree(s->stats);
-    if (s->d_frames) (void)hipFree(s->d_frames);
-    if (s->ev0) (void)hipEventDestroy(s->ev0);
-    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    for (auto &r : s->slots) free_slot(r);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return RT_OK;
@@ -1830,6 +1892,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "grid") s->opt_grid = value;
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
+    else if (k == "inflight") return set_inflight(s, value);
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);
@@ -1862,14 +1925,25 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
     p.rstep = step;
     p.total = (unsigned)((long long)W * nrows);
     p.out = out_rgb;
-    if (hipMemsetAsync(s->work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
-    if (hipMemsetAsync(s->stats, 0, kNStats * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
-    // RT_PROF timeline minima start at all-ones
-    if (hipMemsetAsync(s->stats + 24, 0xff, 2 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
-    (void)hipEventRecord(s->ev0, st);
-    int rc = launch(s, p, st);
-    (void)hipEventRecord(s->ev1, st);
-    s->last_stream = st;
+    RenderSlot &slot = s->slots[(size_t)s->next_slot];
+    s->last_slot = s->next_slot;
+    s->next_slot = (s->next_slot + 1) % (int)s->slots.size();
+    hipStream_t caller = st;
+    if (slot.stream) {                 // several in flight: run on the slot's stream
+        if (hipEventRecord(slot.ev_in, caller) != hipSuccess) return RT_E_HIP;
+        if (hipStreamWaitEvent(slot.stream, slot.ev_in, 0) != hipSuccess) return RT_E_HIP;
+        st = slot.stream;
+    }
+    p.work = slot.work;
+    p.stats = slot.stats;
+    if (hipMemsetAsync(slot.work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
+    if (hipMemsetAsync(slot.stats, 0, kNStats * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    // timeline minima start at all-ones
+    if (hipMemsetAsync(slot.stats + 24, 0xff, 2 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    (void)hipEventRecord(slot.ev0, st);
+    int rc = launch(s, slot, p, st);
+    (void)hipEventRecord(slot.ev1, st);
+    if (slot.stream && hipStreamWaitEvent(caller, slot.ev1, 0) != hipSuccess) return RT_E_HIP;
     s->last_valid = rc == RT_OK;
     return rc;
 }
@@ -1884,9 +1958,10 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     if (!s || !stats) return RT_E_INVALID;
     if (!s->last_valid) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
-    if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
-    unsigned long long h[16];
-    if (hipMemcpy(h, s->stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    const RenderSlot &slot = s->slots[(size_t)s->last_slot];
+    if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
+    unsigned long long h[kNStats];
+    if (hipMemcpy(h, slot.stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
     stats->primary = h[0];
     stats->shadow = h[1];
     stats->refraction = h[2];
@@ -1896,18 +1971,26 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     stats->box_tests = h[6];
     stats->face_tests = h[7];
     stats->sphere_tests = h[8];
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, s->ev0, s->ev1);
-    stats->kernel_ms = ms;
+    // device time of the launch: first wave start .. last wave end (100 MHz
+    // clock); the events' interval also holds any wait for a previous frame
+    // still on the CUs
+    if (h[26] > h[24]) {
+        stats->kernel_ms = (double)(h[26] - h[24]) * 1e-5;
+    } else {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, slot.ev0, slot.ev1);
+        stats->kernel_ms = ms;
+    }
     return RT_OK;
 }
 
 int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     if (!s || !out || n < 0 || n > kNStats || !s->last_valid) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
-    if (hipEventSynchronize(s->ev1) != hipSuccess) return RT_E_HIP;
+    const RenderSlot &slot = s->slots[(size_t)s->last_slot];
+    if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
     unsigned long long h[kNStats];
-    if (hipMemcpy(h, s->stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(h, slot.stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return RT_E_HIP;
     h[16] = (unsigned long long)s->last_mode;
     h[17] = (unsigned long long)s->last_blocks_per_cu;

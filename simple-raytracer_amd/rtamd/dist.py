@@ -28,28 +28,35 @@ def image_rows(H: int, world: int, rank: int, block: int = BLOCK) -> list[int]:
     return [y0 + (k // b) * step + k % b for k in range(nrows)]
 
 
-def alloc_strips(H: int, W: int, world: int, rank: int, device, torch):
-    """This rank's padded row buffer and, on rank 0, the gather targets."""
-    *_, rows_per = row_set(H, world, rank)
-    strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device=device)
-    targets = None
-    if world > 1 and rank == 0:
-        targets = [torch.empty_like(strip) for _ in range(world)]
-    return strip, targets
+class ImageGather:
+    """One frame's row buffer on this rank plus, on rank 0, the gather targets,
+    the full image and the image-order row indices (built once, reused every
+    frame: no host->device index copies in the frame loop)."""
 
+    def __init__(self, H: int, W: int, world: int, rank: int, device, torch):
+        *_, rows_per = row_set(H, world, rank)
+        self.H, self.world, self.rank = H, world, rank
+        self.strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device=device)
+        self.targets = self.image = None
+        self.index = []
+        if world > 1 and rank == 0:
+            self.targets = [torch.empty_like(self.strip) for _ in range(world)]
+            self.image = torch.empty((H, W, 3), dtype=torch.float32, device=device)
+            for r in range(world):
+                rows = image_rows(H, world, r)
+                self.index.append(torch.tensor(rows, dtype=torch.long, device=device) if rows else None)
 
-def gather_strips(strip, targets, world: int, rank: int, H: int, dist, torch):
-    """Collect every rank's rows on rank 0 and put them in image order;
-    returns the H x W x 3 image there (None elsewhere)."""
-    if world == 1:
-        return strip[:H]
-    dist.gather(strip, targets, dst=0)
-    if rank != 0:
-        return None
-    img = torch.empty((H,) + tuple(strip.shape[1:]), dtype=strip.dtype, device=strip.device)
-    for r in range(world):
-        rows = image_rows(H, world, r)
-        if rows:
-            idx = torch.tensor(rows, dtype=torch.long, device=strip.device)
-            img.index_copy_(0, idx, targets[r][: len(rows)])
-    return img
+    def gather(self, dist):
+        """Collect every rank's rows on rank 0 (one fixed-count collective) and
+        put them in image order; returns the H x W x 3 image there (None
+        elsewhere)."""
+        if self.world == 1:
+            return self.strip[: self.H]
+        dist.gather(self.strip, self.targets, dst=0)
+        if self.rank != 0:
+            return None
+        for r, idx in enumerate(self.index):
+            if idx is not None:
+                self.image.index_copy_(0, idx, self.targets[r][: idx.numel()])
+        return self.image
+

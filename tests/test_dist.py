@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import SCENES
-from rtamd.dist import alloc_strips, gather_strips, image_rows, row_set
+from rtamd.dist import ImageGather, image_rows, row_set
 
 
 def _free_port() -> int:
@@ -31,13 +31,14 @@ def _worker(rank, world, port, scene, out_q):
     sc = OracleScene(scene, cwd=SCENES)
     W, H = sc.width, sc.height
     rows = image_rows(H, world, rank)
-    strip, targets = alloc_strips(H, W, world, rank, "cpu", torch)
+    g = ImageGather(H, W, world, rank, "cpu", torch)
     if rows:
         img, _ = sc.render(rows=np.array(rows))
-        strip[: len(rows)] = torch.from_numpy(img)
-    full = gather_strips(strip, targets, world, rank, H, dist, torch)
+        g.strip[: len(rows)] = torch.from_numpy(img)
+    for _ in range(2):                    # buffers are reused frame after frame
+        full = g.gather(dist)
     if rank == 0:
-        out_q.put(full.numpy())
+        out_q.put(full.numpy().copy())
     dist.barrier()
     dist.destroy_process_group()
 

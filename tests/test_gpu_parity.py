@@ -183,6 +183,44 @@ def test_render_into_device_memory():
     assert st2.rays() == st.rays() and st2.kernel_ms > 0
 
 
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_frames_in_flight(inflight):
+    """Option "inflight": renders issued on different caller streams run on the
+    scene's render slots and overlap.  Every frame equals the one-at-a-time
+    render bit for bit, its counters are its own, and work queued on a caller
+    stream after a render sees the finished image."""
+    torch = pytest.importorskip("torch")
+    hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
+    hs.set_depth(4)
+    W, H = hs.width, hs.height
+    cam = hs.camera()
+    gs = rtamd.GpuScene(hs)
+    ref, st = gs.render_rows(cam, W, H, 0, H)
+    gs.set_option("inflight", inflight)
+    streams = [torch.cuda.Stream() for _ in range(inflight)]
+    frames = 2 * inflight + 1
+    outs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(frames)]
+    sums = []
+    for k in range(frames):
+        s = streams[k % inflight]
+        with torch.cuda.stream(s):
+            gs.render_rows_async(cam, W, H, 0, H, outs[k].data_ptr(), s.cuda_stream)
+            sums.append(torch.nan_to_num(outs[k], nan=0.0).sum())   # ordered after the render
+    st2 = gs.last_stats()
+    torch.cuda.synchronize()
+    want = float(np.nan_to_num(ref, nan=0.0).astype(np.float64).sum())
+    for k in range(frames):
+        assert np.array_equal(np.nan_to_num(outs[k].cpu().numpy(), nan=-9), np.nan_to_num(ref, nan=-9)), k
+        assert abs(float(sums[k]) - want) <= 1e-3 * max(1.0, abs(want)), k
+    assert _counts(st2) == _counts(st)
+    assert 0 < st2.kernel_ms < 1000
+    gs.set_option("inflight", 1)
+    img, _ = gs.render_rows(cam, W, H, 0, H)
+    assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9))
+    with pytest.raises(rtamd.RTError):
+        gs.set_option("inflight", 5)
+
+
 def test_abi_errors():
     L = rtamd.hip_lib()
     import ctypes as C
