@@ -1299,21 +1299,29 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         }
         if (!pending) q.tmin = kInf;                 // lane sits this scan out
         if (__ballot(pending) == 0ull) break;
+        // A shadow ray whose cumulative mask (main.cpp:788, carried across the
+        // lights) is already exactly 0 keeps it 0 whatever it hits: every
+        // factor is in [0, 1] when none is NaN (shadow_early_out), and
+        // clamp01(0 * f) = 0.  It is still a TraceRay call of the reference
+        // (counted above); its result is known without searching.
+        const bool known = pending && !q.closest && p.shadow_early_out && (q.mask.r == 0.0f) &
+                           (q.mask.g == 0.0f) & (q.mask.b == 0.0f);
+        const bool search = pending && !known;
 
         w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
         w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
         w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         if (MODE == MODE_BVH) {
-            q.bf = pending && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+            q.bf = search && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
 #if RT_PROF
             unsigned long long c1 = __builtin_amdgcn_s_memtime();
             pc_shade += c1 - c0;
             pc_iter++;
-            pc_lanes += (unsigned long long)__popcll(__ballot(pending && !q.bf));
+            pc_lanes += (unsigned long long)__popcll(__ballot(search && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (pending && !q.bf) bvh_trace(q, p, stk, hits, cnt);
+            if (search && !q.bf) bvh_trace(q, p, stk, hits, cnt);
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1321,13 +1329,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             unsigned long long c2 = __builtin_amdgcn_s_memtime();
             pc_trace += c2 - c1;
 #endif
-            bool need = pending && q.bf;
+            bool need = search && q.bf;
             if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
 #if RT_PROF
             pc_bf += __builtin_amdgcn_s_memtime() - c2;
 #endif
         } else {
-            scan<SRC_LDS>(q, p, lds_f, lds_s, pending, cnt.ftests, cnt.stests);
+            scan<SRC_LDS>(q, p, lds_f, lds_s, search, cnt.ftests, cnt.stests);
         }
     }
     unsigned long long *st = p.stats;
