@@ -55,6 +55,11 @@ def parse_args():
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight: step k renders on stream k mod F (rt_scene option "
                          "'inflight'), so one frame's tail overlaps the next frame's work")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N>1: nccl (= RCCL over xGMI), gloo only to rehearse "
+                         "the multi-rank data path on one GPU (ranks share device 0)")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 checks the last gathered image bit for bit against one whole-image render")
     ap.add_argument("--out-json", default=None)
     return ap.parse_args()
 
@@ -121,9 +126,13 @@ def main() -> None:
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit("bench.py --gpus N>1 must be launched with torchrun (one process per GPU)")
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     cfg = gen.CONFIGS[args.config]
     sd = os.path.join(scene_dir(), f"rank{rank}")
@@ -132,7 +141,7 @@ def main() -> None:
     hs.set_depth(cfg["depth"])
     W, H = hs.width, hs.height
     cam = hs.camera()
-    gs = rtamd.GpuScene(hs, device=local)
+    gs = rtamd.GpuScene(hs, device=dev)
     for kv in args.option:
         k, v = kv.split("=")
         gs.set_option(k, int(v))
@@ -156,8 +165,7 @@ def main() -> None:
             if nrows > 0:
                 gs.render_row_blocks_async(cam, W, H, ry0, rblock, rstep, nrows, g.strip.data_ptr(),
                                            s.cuda_stream)
-            if world > 1:
-                g.gather(dist)
+            return g.gather(dist)
 
     for k in range(args.warmup):
         step(k)
@@ -168,11 +176,26 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k)
+        last_img = step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    verified = None
+    if args.verify and rank == 0:
+        # the last timed step's image (all ranks' rows, gathered and put back in
+        # image order) against one whole-image render on this device
+        ref = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        vs = rtamd.GpuScene(hs, device=dev)
+        vs.render_rows_async(cam, W, H, 0, H, ref.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        vs.last_stats()
+        torch.cuda.synchronize()
+        a, b = torch.nan_to_num(last_img, nan=-9.0), torch.nan_to_num(ref, nan=-9.0)
+        verified = bool(torch.equal(a, b))
+        vs.close()
+        if not verified:
+            raise SystemExit(f"verify: gathered image differs from the whole-image render in "
+                             f"{int((a != b).any(dim=-1).sum())} pixels")
     st = gs.last_stats()          # counters of the last timed render (identical every step)
     my_rays = st.rays()
     # device time of that launch (first wave start .. last wave end, the
@@ -186,7 +209,7 @@ def main() -> None:
     latency_ms = (time.perf_counter() - lat0) * 1e3
 
     t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms)), latency_ms], dtype=torch.float64,
-                     device="cuda")
+                     device="cuda" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -239,7 +262,8 @@ def main() -> None:
             "config": {"workload": WORKLOADS[args.config], "imsize": [W, H], "spheres": ns,
                        "triangles": nt, "depth": cfg["depth"], "lights": 2,
                        "rays_per_step": int(rays_total), "parallelism": f"interleaved 8-row blocks x{world}"
-                       + (" + RCCL gather" if world > 1 else ""), "frames_in_flight": F},
+                       + ((" + RCCL gather" if args.dist_backend == "nccl" else " + gloo gather (rehearsal, one GPU)")
+                          if world > 1 else ""), "frames_in_flight": F},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic, "kernel": "render_kernel",
@@ -259,6 +283,7 @@ def main() -> None:
                                  "peak_GBps": PEAK_HBM_GBPS,
                                  "frac": round(alg_bytes / k_s / 1e9 / PEAK_HBM_GBPS, 7)}},
             "cpu_baseline": cpu,
+            "verified": verified,
             "ray_counts": {k: int(getattr(st, k)) for k in ("primary", "shadow", "refraction",
                                                              "reflection", "skip_trans", "ub_back")},
         }

@@ -35,7 +35,7 @@ class ImageGather:
 
     def __init__(self, H: int, W: int, world: int, rank: int, device, torch):
         *_, rows_per = row_set(H, world, rank)
-        self.H, self.world, self.rank = H, world, rank
+        self.H, self.world, self.rank, self.torch = H, world, rank, torch
         self.strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device=device)
         self.targets = self.image = None
         self.index = []
@@ -52,7 +52,16 @@ class ImageGather:
         elsewhere)."""
         if self.world == 1:
             return self.strip[: self.H]
-        dist.gather(self.strip, self.targets, dst=0)
+        if self.strip.is_cuda and dist.get_backend() == "gloo":
+            # gloo (rehearsal of the multi-rank path on one GPU): host staging
+            cpu = self.strip.cpu()
+            tg = [self.torch.empty_like(cpu) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(cpu, tg, dst=0)
+            if self.rank == 0:
+                for r in range(self.world):
+                    self.targets[r].copy_(tg[r])
+        else:
+            dist.gather(self.strip, self.targets, dst=0)
         if self.rank != 0:
             return None
         for r, idx in enumerate(self.index):
