@@ -165,7 +165,7 @@ inline void collapse4(const Result &R, Result4 &Q) { collapse<4>(R, Q); }
 template <int W>
 struct NodeQBody {
     float origin[3];
-    uint8_t exp[4];          // biased (+127) exponents of the x, y, z scales; [3] unused
+    int8_t exp[4];           // exponents e of the x, y, z scales 2^e (-126 <= e <= kQExpMax); [3] unused
     uint32_t qlo[3][W / 4];  // per axis: lower bounds
     uint32_t qhi[3][W / 4];  // per axis: upper bounds
     int32_t link[W];
@@ -181,8 +181,12 @@ using Node8Q = NodeQ<8>;
 static_assert(sizeof(Node4Q) == 64, "quantised node4 layout");
 static_assert(sizeof(Node8Q) == 96, "quantised node8 layout");
 
-// Returns false if a child box is not finite (NaN/inf geometry): the caller
-// then uses the brute-force scan.
+// Largest scale exponent: the device forms 2^e * (1/d) with |1/d| capped at
+// 2^100, which stays finite for e <= 27 (node extents up to 255 * 2^27).
+constexpr int kQExpMax = 27;
+
+// Returns false if a child box is not finite (NaN/inf geometry) or a node is
+// too large for kQExpMax: the caller then uses the brute-force scan.
 template <int W>
 inline bool quantize(const ResultW<W> &Q, std::vector<NodeQ<W>> &out) {
     out.assign(Q.nodes.size(), NodeQ<W>{});
@@ -208,7 +212,8 @@ inline bool quantize(const ResultW<W> &Q, std::vector<NodeQ<W>> &out) {
             double ext = hi - lo;
             int e = -126;
             while (e < 127 && std::ldexp(255.0, e) < ext) e++;
-            z.exp[a] = (uint8_t)(e + 127);
+            if (e > kQExpMax) return false;
+            z.exp[a] = (int8_t)e;
             double sc = std::ldexp(1.0, e);
             for (int w = 0; w < W / 4; w++) z.qlo[a][w] = z.qhi[a][w] = 0;
             for (int i = 0; i < W; i++) {

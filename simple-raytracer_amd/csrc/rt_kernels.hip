@@ -402,7 +402,13 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 // code runs with most lanes active instead of in almost every wave trip (+6 %
 // over an if-if loop).  The result does not depend on the visiting order.
 __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
-    const float ix = safe_rcp(q.d.x), iy = safe_rcp(q.d.y), iz = safe_rcp(q.d.z);
+    // |1/d| capped at 2^100 (1/0 -> 1e30 as before): the quantised planes'
+    // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
+    // and the cap is conservative: an axis with |d| < 2^-100 moves the ray by
+    // less than 2^-100 D along it, far inside the 2^-16 D primitive padding
+    const float ix = clampr(safe_rcp(q.d.x), -0x1p100f, 0x1p100f);
+    const float iy = clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
+    const float iz = clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
@@ -479,11 +485,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     // the rounding (~ulp(D) in distance) is far inside the primitive padding.
     auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3) {
         float thi = thi_now();
-        unsigned ex = __float_as_uint(w0.w);
-        // 2^e * (1/d): exact power-of-two scaling, kept finite (1/d can be 1e30)
-        float Ax = clampr(__uint_as_float((ex & 0xffu) << 23) * ix, -kFltMax, kFltMax);
-        float Ay = clampr(__uint_as_float(((ex >> 8) & 0xffu) << 23) * iy, -kFltMax, kFltMax);
-        float Az = clampr(__uint_as_float(((ex >> 16) & 0xffu) << 23) * iz, -kFltMax, kFltMax);
+        // 2^e * (1/d): exact power-of-two scaling (one v_bfe_i32 + v_ldexp per
+        // axis; signed exponents in bytes 0..2 of w0.w), finite by the caps
+        const int ex = __float_as_int(w0.w);
+        float Ax = __builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8));
+        float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
+        float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
         float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
         unsigned qlx = __float_as_uint(w1.x), qly = __float_as_uint(w1.y), qlz = __float_as_uint(w1.z);
         unsigned qhx = __float_as_uint(w1.w), qhy = __float_as_uint(w2.x), qhz = __float_as_uint(w2.y);
@@ -510,10 +517,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
 #endif
         cnt.boxes += 8;
         float thi = thi_now();
-        unsigned ex = __float_as_uint(w0.w);
-        float Ax = clampr(__uint_as_float((ex & 0xffu) << 23) * ix, -kFltMax, kFltMax);
-        float Ay = clampr(__uint_as_float(((ex >> 8) & 0xffu) << 23) * iy, -kFltMax, kFltMax);
-        float Az = clampr(__uint_as_float(((ex >> 16) & 0xffu) << 23) * iz, -kFltMax, kFltMax);
+        const int ex = __float_as_int(w0.w);
+        float Ax = __builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8));
+        float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
+        float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
         float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
         const unsigned qlx[2] = {__float_as_uint(w1.x), __float_as_uint(w1.y)};
         const unsigned qly[2] = {__float_as_uint(w1.z), __float_as_uint(w1.w)};

@@ -1,9 +1,10 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 200 python bench.py --steps 3 --cpu-baseline off --verify > gpurun_out/v1.json
-python -c "import json;d=json.load(open('gpurun_out/v1.json'));print(1, d['value'], d['verified'])"
-for n in 2 3; do
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2951$n bench.py --gpus $n --steps 3 --warmup 1 --dist-backend gloo --verify --cpu-baseline off > gpurun_out/v$n.json 2> gpurun_out/v$n.err
-python -c "import json;d=json.loads(open('gpurun_out/v$n.json').read().strip().splitlines()[-1]);print($n, d['value'], d['verified'], d['config']['parallelism'])"
+timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+for v in base cur base cur; do
+  if [ $v = base ]; then L=simple-raytracer_amd/lib_base; else L=simple-raytracer_amd/lib; fi
+  RTAMD_LIB_DIR=$L timeout -k 10 120 python bench.py --cpu-baseline off --steps 10 > gpurun_out/ab.json
+  python -c "import json;d=json.load(open('gpurun_out/ab.json'));print('$v', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])"
 done

@@ -80,7 +80,7 @@ static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int
         if (!quantize<W>(Q, QQ)) { printf("FAIL quantize4\n"); return 1; }
         for (size_t k = 0; k < Q.nodes.size(); k++)
             for (int a = 0; a < 3; a++) {
-                double sc = std::ldexp(1.0, (int)QQ[k].exp[a] - 127), o = QQ[k].origin[a];
+                double sc = std::ldexp(1.0, (int)QQ[k].exp[a]), o = QQ[k].origin[a];
                 for (int i = 0; i < W; i++) {
                     unsigned l = (QQ[k].qlo[a][i / 4] >> (8 * (i % 4))) & 255, h = (QQ[k].qhi[a][i / 4] >> (8 * (i % 4))) & 255;
                     if (Q.nodes[k].link[i] == kEmpty || !(Q.nodes[k].lo[a][i] <= Q.nodes[k].hi[a][i])) {
