@@ -409,6 +409,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     const float ix = clampr(safe_rcp(q.d.x), -0x1p100f, 0x1p100f);
     const float iy = clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
     const float iz = clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
+    [[maybe_unused]] const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
@@ -495,15 +496,21 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         unsigned qlx = __float_as_uint(w1.x), qly = __float_as_uint(w1.y), qlz = __float_as_uint(w1.z);
         unsigned qhx = __float_as_uint(w1.w), qhy = __float_as_uint(w2.x), qhz = __float_as_uint(w2.y);
         int4 lk = make_int4(__float_as_int(w2.z), __float_as_int(w2.w), __float_as_int(w3.x), __float_as_int(w3.y));
+        // near / far plane per axis by the ray's octant: t(q) = fma(q, A, B) is
+        // monotonic in q with the sign of A (= the sign of 1/d), so
+        // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10
+        const unsigned nx = neg_x ? qhx : qlx, fx = neg_x ? qlx : qhx;
+        const unsigned ny = neg_y ? qhy : qly, fy = neg_y ? qly : qhy;
+        const unsigned nz = neg_z ? qhz : qlz, fz = neg_z ? qlz : qhz;
         float tn[4], tf[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int sh = 8 * i;
-            float t0x = fmaf((float)((qlx >> sh) & 0xffu), Ax, Bx), t1x = fmaf((float)((qhx >> sh) & 0xffu), Ax, Bx);
-            float t0y = fmaf((float)((qly >> sh) & 0xffu), Ay, By), t1y = fmaf((float)((qhy >> sh) & 0xffu), Ay, By);
-            float t0z = fmaf((float)((qlz >> sh) & 0xffu), Az, Bz), t1z = fmaf((float)((qhz >> sh) & 0xffu), Az, Bz);
-            tn[i] = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tlo));
-            tf[i] = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
+            float tnx = fmaf((float)((nx >> sh) & 0xffu), Ax, Bx), tfx = fmaf((float)((fx >> sh) & 0xffu), Ax, Bx);
+            float tny = fmaf((float)((ny >> sh) & 0xffu), Ay, By), tfy = fmaf((float)((fy >> sh) & 0xffu), Ay, By);
+            float tnz = fmaf((float)((nz >> sh) & 0xffu), Az, Bz), tfz = fmaf((float)((fz >> sh) & 0xffu), Az, Bz);
+            tn[i] = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
+            tf[i] = fminf(fminf(tfx, tfy), fminf(tfz, thi));
         }
         descend(tn[0], tf[0], tn[1], tf[1], tn[2], tf[2], tn[3], tf[3], lk);
     };
