@@ -416,7 +416,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     int win = -1;
     int nh = 0;
     bool opaque = false;
-    int sp = 0;
+    // stack entry 0 holds kEmpty for good (written once per kernel): popping
+    // the empty stack yields kEmpty with no bounds test
+    int sp = 1;
     int node = rtbvh::kEmpty;                  // >= 0 inner node, < 0 leaf, kEmpty: done
     int leaf = rtbvh::kEmpty;                  // postponed leaf
     // One 4-wide node (rt_bvh.h Node4: lo.x/y/z rows, hi.x/y/z rows, links):
@@ -452,17 +454,22 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         RT_CSWAP(k1, c1, k3, c3);
         RT_CSWAP(k1, c1, k2, c2);
 #undef RT_CSWAP
-        if (k3 < kInf) stk[(sp++) * kBlock] = c3;
-        if (k2 < kInf) stk[(sp++) * kBlock] = c2;
-        if (k1 < kInf) stk[(sp++) * kBlock] = c1;
+        // branch-free pushes: a missed child is written above the top and not
+        // counted (the LDS stack has one spare entry for it)
+        stk[sp * kBlock] = c3;
+        sp += k3 < kInf ? 1 : 0;
+        stk[sp * kBlock] = c2;
+        sp += k2 < kInf ? 1 : 0;
+        stk[sp * kBlock] = c1;
+        sp += k1 < kInf ? 1 : 0;
         if (k0 < kInf) {
             node = c0;
         } else {
-            node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            node = stk[(--sp) * kBlock];
         }
         if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
             leaf = node;                       // park it, keep descending
-            node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            node = stk[(--sp) * kBlock];
         }
     };
     auto thi_now = [&] {
@@ -566,16 +573,18 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         RT_CSWAP8(1, 2) RT_CSWAP8(3, 4) RT_CSWAP8(5, 6)
 #undef RT_CSWAP8
 #pragma unroll
-        for (int i = 7; i >= 1; i--)
-            if (k[i] < kInf) stk[(sp++) * kBlock] = c[i];
+        for (int i = 7; i >= 1; i--) {
+            stk[sp * kBlock] = c[i];
+            sp += k[i] < kInf ? 1 : 0;
+        }
         if (k[0] < kInf) {
             node = c[0];
         } else {
-            node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            node = stk[(--sp) * kBlock];
         }
         if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
             leaf = node;                       // park it, keep descending
-            node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+            node = stk[(--sp) * kBlock];
         }
     };
 #endif
@@ -643,7 +652,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             }
             if (node < 0 && node != rtbvh::kEmpty) {
                 leaf = node;
-                node = sp ? stk[(--sp) * kBlock] : rtbvh::kEmpty;
+                node = stk[(--sp) * kBlock];
             }
         }
         if (node == rtbvh::kEmpty) break;
@@ -1236,6 +1245,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: hits[k * kBlock], k < kHits
     int *stk = hits + kHits * kBlock;                       //           stack[k * kBlock]
+    if (MODE == MODE_BVH) stk[0] = rtbvh::kEmpty;           // bvh_trace's stack bottom (never overwritten)
     Query q;
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
@@ -1479,7 +1489,7 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
     if (mode == MODE_BVH)
-        return (size_t)(kHits + std::max(1, s->bvh_stack)) * kBlock * sizeof(int);
+        return (size_t)(kHits + s->bvh_stack + 2) * kBlock * sizeof(int);   // + sentinel + spare
     return 0;
 }
 
