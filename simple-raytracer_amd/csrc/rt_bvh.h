@@ -73,6 +73,9 @@ inline int32_t leaf_link(int first, int count) { return -(1 + ((first << 4) | co
 // collapsing the binary tree (each node absorbs grandchildren, largest surface
 // area first).
 constexpr int32_t kEmpty = INT32_MIN;
+// Device form of an unused slot: a leaf with no primitives (leaf_records'
+// encoding with offset 0, count 0), so the traversal needs no link test.
+constexpr int32_t kEmptyLeaf = -1;
 template <int W>
 struct NodeW {
     float lo[3][W];

@@ -435,10 +435,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
 #endif
         cnt.boxes += 4;
         // entry distance of each hit child, +inf for a miss or an empty slot
-        float k0 = ((n0 <= f0) & (lk.x != rtbvh::kEmpty)) ? n0 : kInf;
-        float k1 = ((n1 <= f1) & (lk.y != rtbvh::kEmpty)) ? n1 : kInf;
-        float k2 = ((n2 <= f2) & (lk.z != rtbvh::kEmpty)) ? n2 : kInf;
-        float k3 = ((n3 <= f3) & (lk.w != rtbvh::kEmpty)) ? n3 : kInf;
+        // (unused slots link to the empty leaf, kEmptyLeaf: entering one is
+        // harmless, so no link test; their inverted boxes miss anyway)
+        float k0 = (n0 <= f0) ? n0 : kInf;
+        float k1 = (n1 <= f1) ? n1 : kInf;
+        float k2 = (n2 <= f2) ? n2 : kInf;
+        float k3 = (n3 <= f3) ? n3 : kInf;
         int c0 = lk.x, c1 = lk.y, c2 = lk.z, c3 = lk.w;
         // near-first order: 5-comparator sorting network, registers only
 #define RT_CSWAP(ka, ca, kb, cb)                 \
@@ -1633,9 +1635,15 @@ int build_bvh(rt_scene *s, double D) {
 #if RT_QNODE
     std::vector<rtbvh::NodeQ<RT_BVH_WIDTH>> QQ;
     if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ)) ok = false;     // non-finite geometry: scan
+    for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
+        for (auto &l : z.link)
+            if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
     const void *nodes = QQ.data();
     size_t node_bytes = QQ.size() * sizeof(QQ[0]);
 #else
+    for (auto &z : Q.nodes)
+        for (auto &l : z.link)
+            if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
     const void *nodes = Q.nodes.data();
     size_t node_bytes = Q.nodes.size() * sizeof(rtbvh::Node4);
 #endif
