@@ -158,6 +158,10 @@ def main() -> None:
         gs.set_option("inflight", F)
     gathers = [ImageGather(H, W, world, rank, "cuda", torch) for _ in range(F)]
     streams = [torch.cuda.Stream() for _ in range(F)]
+    for s in streams:                     # bind each stream to its hardware queue before timing
+        with torch.cuda.stream(s):
+            gathers[0].strip[:1].zero_()
+    torch.cuda.synchronize()
 
     def step(k):
         s, g = streams[k % F], gathers[k % F]

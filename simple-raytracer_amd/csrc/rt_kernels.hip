@@ -1524,11 +1524,16 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
 #if RT_GLOBAL_FRAMES
     size_t fbytes = (size_t)grid * kBlock * MAXF * sizeof(Frame<MAXF>);
     if (slot.frames_cap < fbytes) {
-        if (slot.d_frames) (void)hipFree(slot.d_frames);
-        slot.d_frames = nullptr;
-        slot.frames_cap = 0;
-        if (hipMalloc(&slot.d_frames, fbytes) != hipSuccess) return hipErrorOutOfMemory;
-        slot.frames_cap = fbytes;
+        // (re)size every slot's buffer now, not each at its first use: a
+        // frame pipeline then allocates once, in its first (warm-up) frame
+        for (RenderSlot &r : s->slots) {
+            if (r.frames_cap >= fbytes) continue;
+            if (r.d_frames) (void)hipFree(r.d_frames);
+            r.d_frames = nullptr;
+            r.frames_cap = 0;
+            if (hipMalloc(&r.d_frames, fbytes) != hipSuccess) return hipErrorOutOfMemory;
+            r.frames_cap = fbytes;
+        }
     }
     pl.frames = slot.d_frames;
 #endif
@@ -1738,6 +1743,11 @@ int set_inflight(rt_scene *s, long long n) {
     for (auto &r : s->slots) {
         int rc = init_slot(r, n > 1);
         if (rc) return rc;
+        // HIP binds a stream to a hardware queue at its first command: do it
+        // here, not in the first frame that uses the slot
+        if (r.stream && (hipMemsetAsync(r.work, 0, sizeof(unsigned), r.stream) != hipSuccess ||
+                         hipStreamSynchronize(r.stream) != hipSuccess))
+            return RT_E_HIP;
     }
     return RT_OK;
 }
