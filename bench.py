@@ -52,9 +52,13 @@ def parse_args():
                     help="cpu_baseline: the reference renders the same scene at NxN")
     ap.add_argument("--option", action="append", default=[],
                     help="kernel option key=value (rt_scene_set_option)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: step k renders on stream k mod F (rt_scene option "
-                         "'inflight'), so one frame's tail overlaps the next frame's work")
+                         "'inflight'), so one frame's tail overlaps the next frame's work; "
+                         "0 = 2 at N=1, 3 at N>1 (frame k+2 must not wait for frame k's gather)")
+    ap.add_argument("--reserve", type=int, default=-1,
+                    help="block slots the persistent render leaves free (rt_scene option 'reserve'); "
+                         "-1 = 0 at N=1, 8 at N>1 (room for the RCCL gather beside the next frame)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1: nccl (= RCCL over xGMI), gloo only to rehearse "
                          "the multi-rank data path on one GPU (ranks share device 0)")
@@ -153,7 +157,10 @@ def main() -> None:
     # F frames in flight: frame k renders into buffer k mod F, ordered on
     # stream k mod F (the render on a library stream of its own, the gather
     # after it); frame k+1 on the next stream overlaps frame k's tail.
-    F = max(1, min(4, args.inflight))
+    F = max(1, min(4, args.inflight if args.inflight > 0 else (2 if world == 1 else 3)))
+    reserve = args.reserve if args.reserve >= 0 else (0 if world == 1 else 8)
+    if reserve:
+        gs.set_option("reserve", reserve)
     if F > 1:
         gs.set_option("inflight", F)
     gathers = [ImageGather(H, W, world, rank, "cuda", torch) for _ in range(F)]
@@ -267,7 +274,8 @@ def main() -> None:
                        "triangles": nt, "depth": cfg["depth"], "lights": 2,
                        "rays_per_step": int(rays_total), "parallelism": f"interleaved 8-row blocks x{world}"
                        + ((" + RCCL gather" if args.dist_backend == "nccl" else " + gloo gather (rehearsal, one GPU)")
-                          if world > 1 else ""), "frames_in_flight": F},
+                          if world > 1 else ""), "frames_in_flight": F,
+                       "reserved_block_slots": reserve},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic, "kernel": "render_kernel",

@@ -160,7 +160,9 @@ int rt_render_row_blocks_async(rt_scene *scene, const rt_camera *cam, int W, int
 
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
- * (persistent blocks, 0 = occupancy), "depth" (recursion depth override),
+ * (persistent blocks, 0 = occupancy), "reserve" (block slots the occupancy-
+ * sized grid leaves free, e.g. for a collective's kernel that must run beside
+ * a persistent render), "depth" (recursion depth override),
  * "inflight" (1..4, default 1: renders of this scene that may run at once.
  * With n > 1 each render gets its own work counter, counters and ShadeRay
  * frame buffer and runs on a library stream, ordered against its caller's

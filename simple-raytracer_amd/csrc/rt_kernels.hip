@@ -1458,6 +1458,7 @@ struct rt_scene {
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
+    long long opt_reserve = 0;         // occupancy-derived grid: block slots left free for other kernels
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
     long long opt_bvh_leaf = 8;        // SAH max leaf size
     long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
@@ -1516,7 +1517,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     int nb = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE>, kBlock, shm);
     if (nb < 1) nb = 1;
-    long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu;
+    long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu - s->opt_reserve;
     long long need = ((long long)p.total + kBlock - 1) / kBlock;
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
@@ -1955,6 +1956,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     std::string k(key);
     if (k == "lds") s->opt_lds = value;
     else if (k == "grid") s->opt_grid = value;
+    else if (k == "reserve") s->opt_reserve = std::max(0LL, value);
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
     else if (k == "inflight") return set_inflight(s, value);

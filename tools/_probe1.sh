@@ -1,7 +1,11 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for a in "--config C2 --steps 3" "--config C2 --steps 20" "--config C2 --steps 20 --inflight 1" "--steps 5" "--steps 20"; do
-  timeout -k 10 300 python bench.py $a --cpu-baseline off > gpurun_out/b.json
-  python -c "import json;d=json.load(open('gpurun_out/b.json'));print('$a', d['value'], d['ms_per_step'], d['frame_latency_ms'], d['roofline']['kernel_ms'])"
+timeout -k 10 200 python bench.py --steps 10 --cpu-baseline off --verify > gpurun_out/v1.json
+python -c "import json;d=json.load(open('gpurun_out/v1.json'));print(1, d['value'], d['verified'], d['config']['frames_in_flight'])"
+timeout -k 10 200 python bench.py --steps 10 --cpu-baseline off --inflight 3 --reserve 8 > gpurun_out/v1b.json
+python -c "import json;d=json.load(open('gpurun_out/v1b.json'));print('1 f3 r8', d['value'])"
+for n in 2 4; do
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2952$n bench.py --gpus $n --steps 4 --warmup 1 --dist-backend gloo --verify --cpu-baseline off > gpurun_out/v$n.json 2> gpurun_out/v$n.err
+python -c "import json;d=json.loads(open('gpurun_out/v$n.json').read().strip().splitlines()[-1]);print($n, d['value'], d['verified'], d['config']['frames_in_flight'], d['config']['reserved_block_slots'])"
 done
