@@ -158,6 +158,11 @@ int rt_scene_last_stats(rt_scene *scene, rt_stats *stats);
 int rt_render_row_blocks_async(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,
                                int nrows, float *out_rgb, void *hip_stream);
 
+/* Synchronous form of rt_render_row_blocks_async: out_rgb (nrows * W * 3
+ * floats) may be host or device memory.  stats may be NULL. */
+int rt_render_row_blocks(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,
+                         int nrows, float *out_rgb, rt_stats *stats);
+
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
  * (persistent blocks, 0 = occupancy), "reserve" (block slots the occupancy-

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <iostream>
 #include <stdexcept>
 #include <string>
@@ -72,12 +73,31 @@ int main(int argc, char *argv[]) {
     std::vector<rt_stats> st(gpus);
     std::vector<int> rcs(gpus, 0);
     std::vector<std::thread> pool;
+    // One host thread per device.  One device renders the image in one call;
+    // several deal the rows out in 8-row blocks, round robin (device g gets
+    // blocks g, g+N, ...: every device the same mix of cheap and costly rows),
+    // each renders its row set into a buffer of its own and the blocks are
+    // put back in image order.
+    const int kRowBlock = 8;
     for (int g = 0; g < gpus; g++) {
         pool.emplace_back([&, g] {
-            int y0 = (int)((long long)H * g / gpus), y1 = (int)((long long)H * (g + 1) / gpus);
             rt_scene *s = nullptr;
             int r = rt_scene_create(device + g, rth_desc(hs), &s);
-            if (!r) r = rt_render_rows(s, &cam, W, H, y0, y1, img.data() + (size_t)y0 * W * 3, &st[g]);
+            if (!r && gpus == 1) {
+                r = rt_render_rows(s, &cam, W, H, 0, H, img.data(), &st[g]);
+            } else if (!r) {
+                std::vector<int> rows;
+                for (int b = g * kRowBlock; b < H; b += gpus * kRowBlock)
+                    for (int y = b; y < std::min(H, b + kRowBlock); y++) rows.push_back(y);
+                if (!rows.empty()) {
+                    std::vector<float> part(rows.size() * (size_t)W * 3);
+                    r = rt_render_row_blocks(s, &cam, W, H, g * kRowBlock, kRowBlock, gpus * kRowBlock,
+                                             (int)rows.size(), part.data(), &st[g]);
+                    for (size_t k = 0; !r && k < rows.size(); k++)
+                        std::copy(part.begin() + k * (size_t)W * 3, part.begin() + (k + 1) * (size_t)W * 3,
+                                  img.begin() + (size_t)rows[k] * W * 3);
+                }
+            }
             rt_scene_destroy(s);
             rcs[g] = r;
         });

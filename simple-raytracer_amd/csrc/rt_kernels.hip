@@ -2073,6 +2073,12 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
 
 int rt_render_rows(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb, rt_stats *stats) {
     if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || y1 > H || y0 >= y1) return RT_E_INVALID;
+    return rt_render_row_blocks(s, cam, W, H, y0, y1 - y0, y1 - y0, y1 - y0, out_rgb, stats);
+}
+
+int rt_render_row_blocks(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int block, int step, int nrows,
+                         float *out_rgb, rt_stats *stats) {
+    if (!s || !cam || !out_rgb || nrows < 1) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     hipPointerAttribute_t attr;
     bool on_device = false;
@@ -2080,7 +2086,7 @@ int rt_render_rows(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int 
         on_device = attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
     else
         (void)hipGetLastError();
-    size_t bytes = (size_t)W * (size_t)(y1 - y0) * 3 * sizeof(float);
+    size_t bytes = (size_t)W * (size_t)nrows * 3 * sizeof(float);
     float *dst = out_rgb;
     if (!on_device) {
         if (s->dev_out_bytes < bytes) {
@@ -2092,7 +2098,7 @@ int rt_render_rows(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int 
         }
         dst = s->dev_out;
     }
-    int rc = rt_render_rows_async(s, cam, W, H, y0, y1, dst, nullptr);
+    int rc = rt_render_row_blocks_async(s, cam, W, H, y0, block, step, nrows, dst, nullptr);
     if (rc) return rc;
     if (!on_device && hipMemcpyAsync(out_rgb, dst, bytes, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
         return RT_E_HIP;

@@ -86,7 +86,8 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
                 "rth_output_path"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
-               "rt_render_rows_async", "rt_render_row_blocks_async", "rt_scene_last_stats",
+               "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks",
+               "rt_scene_last_stats",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_strerror"]
 
 
@@ -139,6 +140,8 @@ def hip_lib() -> C.CDLL:
         L.rt_render_row_blocks_async.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int,
                                                  C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                                  C.c_void_p]
+        L.rt_render_row_blocks.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
+                                           C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
@@ -294,6 +297,18 @@ class GpuScene:
         _check(hip_lib().rt_render_row_blocks_async(self._h, C.byref(cam), W, H, y0, block, step, nrows,
                                                     C.c_void_p(dev_ptr), C.c_void_p(stream or 0)),
                "rt_render_row_blocks_async")
+
+    def render_row_blocks(self, cam: rt_camera, W: int, H: int, y0: int, block: int, step: int, nrows: int,
+                          out=None):
+        """Synchronous block-interleaved row set into a numpy array (host):
+        local row k is image row y0 + (k // block) * step + k % block."""
+        st = rt_stats()
+        if out is None:
+            out = np.empty((nrows, W, 3), dtype=np.float32)
+        _check(hip_lib().rt_render_row_blocks(self._h, C.byref(cam), W, H, y0, block, step, nrows,
+                                              C.c_void_p(out.ctypes.data), C.byref(st)),
+               "rt_render_row_blocks")
+        return out, st
 
     def last_stats(self) -> rt_stats:
         st = rt_stats()

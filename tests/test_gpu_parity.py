@@ -166,6 +166,16 @@ def test_row_blocks_reassemble(world):
         img[image_rows(H, world, r)] = buf[:n].cpu().numpy()
     assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(full, nan=-9))
     assert rays == st.rays()
+    # the synchronous entry point into host memory (the CLI's multi-device path)
+    img2 = np.zeros_like(full)
+    rays = 0
+    for r in range(world):
+        y0, b, step, n, per = row_set(H, world, r)
+        part, s = gs.render_row_blocks(cam, W, H, y0, b, step, n)
+        rays += s.rays()
+        img2[image_rows(H, world, r)] = part
+    assert np.array_equal(np.nan_to_num(img2, nan=-9), np.nan_to_num(full, nan=-9))
+    assert rays == st.rays()
 
 
 def test_render_into_device_memory():
