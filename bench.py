@@ -105,6 +105,29 @@ def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
             "sample": f"{config} scene at {sample}x{sample}, oracle restatement, {dt:.1f} s"}
 
 
+def cpu_port_baseline(config: str, sample: int) -> dict:
+    """SURVEY.md §8d's CPU path: this repo's C restatement of the reference
+    (oracle/rt_oracle.c: the same brute-force TraceRay/ShadeRay), OpenMP over
+    rows on all the threads this process may use (OMP_NUM_THREADS), timed on a
+    sample x sample render of the same seeded scene.  A reported baseline, not
+    the product (the product path has no CPU fallback)."""
+    from rtamd import scenes as gen
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleScene
+    d = tempfile.mkdtemp(prefix="rtamd_port_")
+    path = gen.write_scene(d, config, w=sample, h=sample, tag=f"{config}_{sample}_port")
+    o = OracleScene(path)
+    o.set_depth(gen.CONFIGS[config]["depth"])
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    t0 = time.perf_counter()
+    _, cnt = o.render(threads=threads)
+    dt = time.perf_counter() - t0
+    r = sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection"))
+    return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{config} scene at {sample}x{sample} (full field of view), {r} rays, {dt:.1f} s, "
+                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows"}
+
+
 def load_pmc_traffic(config: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -247,7 +270,7 @@ def main() -> None:
         # PMC bytes were collected for a whole-image launch: only the N=1 line's
         # launch is that launch (a rank's strip at N>1 is not measured)
         traffic = load_pmc_traffic(args.config) if world == 1 else None
-        cpu = None
+        cpu = cpu_port = None
         if args.cpu_baseline == "auto" and world == 1:
             def gpu_rays(p):
                 _, s = rtamd.render_scene(p, cwd=os.path.dirname(p), depth=cfg["depth"], device=local)
@@ -256,6 +279,10 @@ def main() -> None:
                 cpu = cpu_baseline(args.config, args.cpu_sample, gpu_rays)
             except Exception as e:  # never lose the GPU line to the CPU leg
                 cpu = {"error": repr(e)}
+            try:
+                cpu_port = cpu_port_baseline(args.config, 2 * args.cpu_sample)
+            except Exception as e:
+                cpu_port = {"error": repr(e)}
         line = {
             "metric": "Mrays/s (primary+secondary)",
             "value": round(value, 3),
@@ -295,6 +322,7 @@ def main() -> None:
                                  "peak_GBps": PEAK_HBM_GBPS,
                                  "frac": round(alg_bytes / k_s / 1e9 / PEAK_HBM_GBPS, 7)}},
             "cpu_baseline": cpu,
+            "cpu_port": cpu_port,
             "verified": verified,
             "ray_counts": {k: int(getattr(st, k)) for k in ("primary", "shadow", "refraction",
                                                              "reflection", "skip_trans", "ub_back")},
