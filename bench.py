@@ -280,7 +280,7 @@ def main() -> None:
             except Exception as e:  # never lose the GPU line to the CPU leg
                 cpu = {"error": repr(e)}
             try:
-                cpu_port = cpu_port_baseline(args.config, 2 * args.cpu_sample)
+                cpu_port = cpu_port_baseline(args.config, 4 * args.cpu_sample)
             except Exception as e:
                 cpu_port = {"error": repr(e)}
         line = {
