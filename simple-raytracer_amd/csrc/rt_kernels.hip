@@ -782,8 +782,11 @@ struct Frame {
     FFloat ei, et;                   // incidence / transmission refraction index
     FV3 P, N, I;                     // hit point, shading normal (flipped for spheres), I = -ray
     FFloat cosI;
-    FC3 dif, mask, acc;              // diffuse, cumulative shadow mask, running colour
+    FC3 dif, acc;                    // diffuse, running colour
     FFloat Ft;                       // transmission Fresnel F (main.cpp:966)
+    // No shadow mask: it starts at {1,1,1} before the light loop (main.cpp:788)
+    // and lives in the shadow query from one light to the next.
+    FInt pad_[MAXF == 5 ? 3 : 1];    // depth 4: the frame is one 128-B line
 };
 
 
@@ -867,7 +870,6 @@ __device__ void node_begin(const Params &p, Frame<MAXF> &f, V3 o, V3 d, float t)
     f.I = I;
     f.cosI = cosI;
     f.dif = dif;
-    f.mask = C3{1.0f, 1.0f, 1.0f};
     f.acc = C3{0.0f, 0.0f, 0.0f};    // tmp_specular while lights run
     f.light = 0;
     f.phase = PH_LIGHT;
@@ -1072,7 +1074,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
             facc = cadd(facc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
             light++;
-            f.mask = q.mask;
             f.acc = facc;
             f.light = light;
             if (light < p.nl) {
@@ -1149,7 +1150,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 q.skipchk = false;
                 q.skipped = false;
                 q.win = -1;
-                q.mask = f.mask;
+                q.mask = C3{1.0f, 1.0f, 1.0f};   // the node's first light (main.cpp:788)
                 ls.top = top;
                 return RK_SHADOW;
             }
