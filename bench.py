@@ -55,7 +55,7 @@ def parse_args():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: step k renders on stream k mod F (rt_scene option "
                          "'inflight'), so one frame's tail overlaps the next frame's work; "
-                         "0 = 2 at N=1, 3 at N>1 (frame k+2 must not wait for frame k's gather)")
+                         "0 = 2 at N=1, 4 at N>1 (a frame never waits for the gather two frames back; an even count keeps consecutive frames on different hardware queues)")
     ap.add_argument("--reserve", type=int, default=-1,
                     help="block slots the persistent render leaves free (rt_scene option 'reserve'); "
                          "-1 = 0 at N=1, 8 at N>1 (room for the RCCL gather beside the next frame)")
@@ -180,7 +180,7 @@ def main() -> None:
     # F frames in flight: frame k renders into buffer k mod F, ordered on
     # stream k mod F (the render on a library stream of its own, the gather
     # after it); frame k+1 on the next stream overlaps frame k's tail.
-    F = max(1, min(4, args.inflight if args.inflight > 0 else (2 if world == 1 else 3)))
+    F = max(1, min(4, args.inflight if args.inflight > 0 else (2 if world == 1 else 4)))
     reserve = args.reserve if args.reserve >= 0 else (0 if world == 1 else 8)
     if reserve:
         gs.set_option("reserve", reserve)
@@ -230,17 +230,18 @@ def main() -> None:
         if not verified:
             raise SystemExit(f"verify: gathered image differs from the whole-image render in "
                              f"{int((a != b).any(dim=-1).sum())} pixels")
-    st = gs.last_stats()          # counters of the last timed render (identical every step)
-    my_rays = st.rays()
-    # device time of that launch (first wave start .. last wave end, the
-    # kernel's own clock; what rocprofv3 reports per dispatch)
-    kernel_ms = [st.kernel_ms]
     # single-frame latency (nothing else in flight), after the timed region
     torch.cuda.synchronize()
     lat0 = time.perf_counter()
     step(0)
     torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - lat0) * 1e3
+    st = gs.last_stats()          # counters of that render (identical every step)
+    my_rays = st.rays()
+    # device time of one launch with no other frame on the CUs (first wave start
+    # .. last wave end on the kernel's own clock; what rocprofv3 reports per
+    # dispatch at --inflight 1)
+    kernel_ms = [st.kernel_ms]
 
     t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms)), latency_ms], dtype=torch.float64,
                      device="cuda" if args.dist_backend == "nccl" else "cpu")

@@ -46,15 +46,23 @@ def main():
     W, H = hs.width, hs.height
     cam = hs.camera()
     y0, b, step, nr, _ = row_set(H, rows[0], rows[1])
-    slots = "--slots" in sys.argv          # one scene, option inflight=2 (render slots)
+    slots = "--slots" in sys.argv          # one scene, option inflight=F (render slots)
+    F = int(os.environ.get("INFLIGHT", "2"))
     if slots:
         g = rtamd.GpuScene(hs)
-        g.set_option("inflight", 2)
-        scenes = [g, g]
+        g.set_option("inflight", F)
+        if "RESERVE" in os.environ:
+            g.set_option("reserve", int(os.environ["RESERVE"]))
+        scenes = [g] * F
     else:
+        F = 2
         scenes = [rtamd.GpuScene(hs), rtamd.GpuScene(hs)]
-    outs = [torch.empty((nr, W, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty((nr, W, 3), dtype=torch.float32, device="cuda") for _ in range(F)]
+    streams = [torch.cuda.Stream() for _ in range(F)]
+    for s_ in streams:
+        with torch.cuda.stream(s_):
+            outs[0][:1].zero_()
+    torch.cuda.synchronize()
 
     own = "--own-streams" in sys.argv       # the scenes' own rt_scene streams
 
@@ -72,13 +80,14 @@ def main():
 
     res = {"config": cfg, "rows": rows, "frames": frames, "mode": "slots" if slots else
            ("own-streams" if own else "two scenes, torch streams")}
-    for nflight in (1, 2, 1, 2):
+    for nflight in (1, F, 1, F):
         run(nflight)                       # warm
         res[f"ms_per_frame_{nflight}"] = round(run(nflight), 3)
     st = scenes[0].last_stats()
     res["single_kernel_ms"] = round(st.kernel_ms, 3)
     res["rays"] = st.rays()
-    torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=0)
+    for o in outs[1:]:
+        torch.testing.assert_close(outs[0], o, rtol=0, atol=0, equal_nan=True)
     print(json.dumps(res))
 
 
