@@ -186,6 +186,7 @@ def main() -> None:
         gs.set_option("reserve", reserve)
     if F > 1:
         gs.set_option("inflight", F)
+    gs.prepare(cam, W, H)                 # BVH + every slot's frame buffer, before any step
     gathers = [ImageGather(H, W, world, rank, "cuda", torch) for _ in range(F)]
     streams = [torch.cuda.Stream() for _ in range(F)]
     for s in streams:                     # bind each stream to its hardware queue before timing

@@ -158,6 +158,11 @@ int rt_scene_last_stats(rt_scene *scene, rt_stats *stats);
 int rt_render_row_blocks_async(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,
                                int nrows, float *out_rgb, void *hip_stream);
 
+/* Optional: build the acceleration structure for this camera and size every
+ * render slot's buffers for a W x H image now, so that no later render pays
+ * for either (the first render would, once).  Renders nothing. */
+int rt_scene_prepare(rt_scene *scene, const rt_camera *cam, int W, int H);
+
 /* Synchronous form of rt_render_row_blocks_async: out_rgb (nrows * W * 3
  * floats) may be host or device memory.  stats may be NULL. */
 int rt_render_row_blocks(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,

@@ -1513,7 +1513,7 @@ size_t mode_lds_bytes(const rt_scene *s, int mode) {
 }
 
 template <int MAXF, int MODE>
-hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_t st) {
+hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_t st, bool dry) {
     size_t shm = mode_lds_bytes(s, MODE);
     int nb = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE>, kBlock, shm);
@@ -1543,15 +1543,16 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     s->last_grid = grid;
     s->last_lds = (long long)shm;
     s->last_mode = MODE;
+    if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
     hipLaunchKernelGGL((render_kernel<MAXF, MODE>), dim3((unsigned)grid), dim3(kBlock), shm, st, pl);
     return hipGetLastError();
 }
 
 template <int MAXF>
-hipError_t launch_mode(rt_scene *s, RenderSlot &slot, const Params &p, int mode, hipStream_t st) {
-    if (mode == MODE_BVH) return launch_one<MAXF, MODE_BVH>(s, slot, p, st);
-    if (mode == MODE_SCAN_LDS) return launch_one<MAXF, MODE_SCAN_LDS>(s, slot, p, st);
-    return launch_one<MAXF, MODE_SCAN>(s, slot, p, st);
+hipError_t launch_mode(rt_scene *s, RenderSlot &slot, const Params &p, int mode, hipStream_t st, bool dry) {
+    if (mode == MODE_BVH) return launch_one<MAXF, MODE_BVH>(s, slot, p, st, dry);
+    if (mode == MODE_SCAN_LDS) return launch_one<MAXF, MODE_SCAN_LDS>(s, slot, p, st, dry);
+    return launch_one<MAXF, MODE_SCAN>(s, slot, p, st, dry);
 }
 
 // Distance bound for the BVH padding: from any ray origin (the eye, or a point
@@ -1673,7 +1674,7 @@ int build_bvh(rt_scene *s, double D) {
     return RT_OK;
 }
 
-int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st) {
+int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = false) {
     int depth = p.depth < 0 ? 0 : p.depth;
     if (depth > 16) return RT_E_UNSUPPORTED;
     int nobj = p.nf + p.ns;
@@ -1698,9 +1699,9 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st) {
         if (lds) mode = MODE_SCAN_LDS;
     }
     hipError_t e;
-    if (depth <= 4) e = launch_mode<5>(s, slot, p, mode, st);
-    else if (depth <= 8) e = launch_mode<9>(s, slot, p, mode, st);
-    else e = launch_mode<17>(s, slot, p, mode, st);
+    if (depth <= 4) e = launch_mode<5>(s, slot, p, mode, st, dry);
+    else if (depth <= 8) e = launch_mode<9>(s, slot, p, mode, st, dry);
+    else e = launch_mode<17>(s, slot, p, mode, st, dry);
     return e == hipSuccess ? RT_OK : RT_E_HIP;
 }
 
@@ -2013,6 +2014,25 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
     (void)hipEventRecord(slot.ev1, st);
     if (slot.stream && hipStreamWaitEvent(caller, slot.ev1, 0) != hipSuccess) return RT_E_HIP;
     s->last_valid = rc == RT_OK;
+    return rc;
+}
+
+int rt_scene_prepare(rt_scene *s, const rt_camera *cam, int W, int H) {
+    if (!s || !cam || W < 2 || H < 2) return RT_E_INVALID;
+    if ((long long)W * H >= (1ll << 31)) return RT_E_UNSUPPORTED;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    Params p = s->base;
+    for (int c = 0; c < 3; c++) {
+        p.eye[c] = cam->eye[c];
+        p.ul[c] = cam->ul[c];
+        p.dh[c] = cam->dh[c];
+        p.dv[c] = cam->dv[c];
+    }
+    p.W = W;
+    p.rows = H;
+    p.total = (unsigned)((long long)W * H);
+    int rc = launch(s, s->slots[0], p, s->stream, true);
+    if (rc == RT_OK && hipDeviceSynchronize() != hipSuccess) rc = RT_E_HIP;
     return rc;
 }
 

@@ -87,7 +87,7 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
                 "rth_output_path"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks",
-               "rt_scene_last_stats",
+               "rt_scene_last_stats", "rt_scene_prepare",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_strerror"]
 
 
@@ -143,6 +143,7 @@ def hip_lib() -> C.CDLL:
         L.rt_render_row_blocks.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                            C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
+        L.rt_scene_prepare.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
@@ -309,6 +310,10 @@ class GpuScene:
                                               C.c_void_p(out.ctypes.data), C.byref(st)),
                "rt_render_row_blocks")
         return out, st
+
+    def prepare(self, cam: rt_camera, W: int, H: int) -> None:
+        """rt_scene_prepare: BVH for this camera + every slot's buffers, no render."""
+        _check(hip_lib().rt_scene_prepare(self._h, C.byref(cam), W, H), "rt_scene_prepare")
 
     def last_stats(self) -> rt_stats:
         st = rt_stats()

@@ -193,6 +193,24 @@ def test_render_into_device_memory():
     assert st2.rays() == st.rays() and st2.kernel_ms > 0
 
 
+def test_prepare_then_render():
+    """rt_scene_prepare builds the BVH and sizes the slots' buffers without
+    rendering; renders after it are unchanged."""
+    hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
+    W, H = hs.width, hs.height
+    cam = hs.camera()
+    ref, st = rtamd.GpuScene(hs).render_rows(cam, W, H, 0, H)
+    gs = rtamd.GpuScene(hs)
+    gs.set_option("inflight", 2)
+    gs.prepare(cam, W, H)
+    gs.prepare(cam, W, H)                     # idempotent
+    img, st2 = gs.render_rows(cam, W, H, 0, H)
+    assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9))
+    assert _counts(st2) == _counts(st)
+    with pytest.raises(rtamd.RTError):
+        gs.prepare(cam, 1, H)
+
+
 @pytest.mark.parametrize("inflight", [2, 3])
 def test_frames_in_flight(inflight):
     """Option "inflight": renders issued on different caller streams run on the
