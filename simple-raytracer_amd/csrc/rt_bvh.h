@@ -304,7 +304,10 @@ inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace
 
 class Builder {
    public:
-    static constexpr int kBins = 32;
+#ifndef RT_SAH_BINS
+#define RT_SAH_BINS 64  // 32 -> 64: box tests -1.2 %, C3 +0.4 % (A/B)
+#endif
+    static constexpr int kBins = RT_SAH_BINS;
     int max_leaf = 8;                       // SAH leaves (<= 15 fits the link encoding)
     float trav_cost = 1.0f;                 // SAH cost of one node visit, in sphere tests
     static constexpr int kSahDepth = 22;    // deeper: object-median splits (bounded depth)
