@@ -299,3 +299,52 @@ def test_cli_drop_in(name, golden, tmp_path):
         ref, _ = o.render()
         q = rtamd.quantize(ref).reshape(-1, 3).astype(np.uint64)
         assert (mine != q).any(axis=1).mean() <= MAX_BAD_FRAC
+
+
+def _render_both(name, cwd, W=None, H=None, accel=None):
+    opts = None if accel is None else {"accel": accel}
+    img, st = rtamd.render_scene(name, cwd=cwd, imsize=(W, H) if W else None, options=opts)
+    ref, cnt = OracleScene(name, cwd=cwd).render(W, H)
+    return img, st, ref, cnt
+
+
+@pytest.mark.parametrize("W,H", [(2, 2), (3, 5), (67, 13), (130, 9), (9, 130)])
+@pytest.mark.parametrize("name,accel", [("Test1.txt", None), ("test7.txt", None), ("_c3_ragged.txt", 1)])
+def test_ragged_image_sizes(name, accel, W, H, tmp_path):
+    """Image sizes that are not multiples of the 8x8 pixel tile (partial
+    tiles, a partial last wave, one-tile-wide images), against the oracle
+    with identical ray counts.  `_c3_ragged` is a C3-style scene (2000
+    objects, reflection + refraction) through the BVH."""
+    cwd = SCENES
+    if name.startswith("_"):
+        cwd = str(tmp_path)
+        open(os.path.join(cwd, name), "w").write(gen.scene_text("C3", w=W, h=H))
+    img, st, ref, cnt = _render_both(name, cwd, W, H, accel)
+    assert img.shape == (H, W, 3)
+    assert_parity(img, ref, f"{name}@{W}x{H}")
+    assert _counts(st) == cnt
+
+
+_HEADER = ("imsize 33 17\neye 0 0 0\nviewdir 0 0 -1\nupdir 0 1 0\nhfov 60\n"
+           "bkgcolor 0.1 0.2 0.3 1\nlight -10 10 0 1 0.6 0.6 0.6\n")
+
+
+@pytest.mark.parametrize("body,kind", [
+    ("", "empty"),                                            # no objects: background only
+    ("mtlcolor 1 0 0 1 1 1 0.2 0.6 0.5 20 0.3 1.5\n"          # a single glass sphere
+     "sphere 0 0 -5 1\n", "one_sphere"),
+    ("mtlcolor 0 1 0 1 1 1 0.2 0.6 0.5 20\n"                  # faces only (no spheres)
+     "v -1 -1 -4\nv 1 -1 -4\nv 0 1 -5\nv 2 1 -6\nf 1 2 3\nf 2 4 3\n", "faces_only"),
+])
+@pytest.mark.parametrize("accel", [0, 1])
+def test_degenerate_scenes(body, kind, accel, tmp_path):
+    """Scenes at the edges of the object counts: nothing to hit, one object,
+    faces without spheres -- both search strategies, against the oracle."""
+    open(os.path.join(tmp_path, "s.txt"), "w").write(_HEADER + body)
+    img, st, ref, cnt = _render_both("s.txt", str(tmp_path), accel=accel)
+    assert img.shape == (17, 33, 3)
+    assert_parity(img, ref, f"{kind} accel{accel}")
+    assert _counts(st) == cnt
+    if kind == "empty":
+        assert np.all(img == np.float32([0.1, 0.2, 0.3]))
+        assert cnt["shadow"] == cnt["reflection"] == cnt["refraction"] == 0
