@@ -889,6 +889,37 @@ int oracle_render_rows(const or_scene *S, int W, int H, const int *rows, int nro
     return 0;
 }
 
+/* Render an arbitrary pixel list (x, y pairs) of a W x H image -- the
+ * full-size row-span samples of the parity tests (main.cpp:718-764 per pixel). */
+int oracle_render_pixels(const or_scene *S, int W, int H, const int *xy, int npx, int threads, float *out,
+                         long long *counts) {
+    camera cam = make_camera(S, W, H);
+    long long tot[6] = {0};
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel num_threads(threads)
+#endif
+    {
+        counters C; memset(&C, 0, sizeof C);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 16)
+#endif
+        for (int k = 0; k < npx; k++) {
+            col c = render_pixel(S, &cam, xy[2 * k + 1], xy[2 * k], &C);
+            out[3 * (size_t)k + 0] = c.r; out[3 * (size_t)k + 1] = c.g; out[3 * (size_t)k + 2] = c.b;
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            tot[0] += C.prim; tot[1] += C.shadow; tot[2] += C.refr; tot[3] += C.refl;
+            tot[4] += C.skip; tot[5] += C.ub_back;
+        }
+    }
+    for (int k = 0; k < 6; k++) counts[k] = tot[k];
+    return 0;
+}
+
 /* main.cpp:760: static_cast<int>(map(c, 0, 1, 0, 255)) on x86-64:
  * cvttss2si yields INT_MIN for NaN and out-of-range values. */
 static int quantize(float c) {

@@ -67,6 +67,11 @@ int main(int argc, char *argv[]) {
         std::cerr << "rt: no HIP device" << std::endl;
         return 2;
     }
+    if (device < 0 || device >= ndev) {
+        std::cerr << "rt: --device " << device << " out of range (" << ndev << " HIP device"
+                  << (ndev == 1 ? "" : "s") << ")" << std::endl;
+        return 2;
+    }
     if (gpus < 1) gpus = 1;
     if (gpus > ndev - device) gpus = ndev - device;
     std::vector<float> img((size_t)W * H * 3);

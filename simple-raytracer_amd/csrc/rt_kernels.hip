@@ -27,6 +27,7 @@
 // powf/acosf/asinf/acos/atan2 differences.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -149,7 +150,7 @@ struct Params {
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int bvh_stack;                       // BVH: LDS stack entries per lane (worst case of the tree)
-    void *__restrict__ frames;           // RT_GLOBAL_FRAMES: grid x kBlock x MAXF ShadeRay frames
+    void *__restrict__ frames;           // grid x kBlock x MAXF ShadeRay frames
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -281,11 +282,9 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 //             traversal order differs from the reference's object order by
 //             rounding only (<= 1 ulp per factor); an opaque
 //             hit zeroes the mask whatever the order (early exit when no
-//             factor is NaN).  RT_ORDERED_SHADOW=1 restores the object order
-//             bit for bit with an LDS key list (kHits entries per lane).
+//             factor is NaN).
 // Queries the BVH cannot reproduce (SKIP_TRANS checks, directional shadow
-// rays against spheres[, > kHits semi-transparent hits when ordered]) set
-// q.bf and are re-run by the brute-force scan.
+// rays against spheres) set q.bf and are re-run by the brute-force scan.
 // ---------------------------------------------------------------------------
 // Per-lane counters kept small (VGPR pressure): ray kinds are counted per
 // wave with ballots in the main loop (scalar registers); only the rare events
@@ -302,41 +301,18 @@ struct Counters {
 };
 enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
-#ifndef RT_ORDERED_SHADOW
-#define RT_ORDERED_SHADOW 0
-#endif
-constexpr int kHits = RT_ORDERED_SHADOW ? 8 : 0;
-#ifndef RT_QNODE
-#define RT_QNODE 1                       // 1: quantised nodes (rt_bvh.h NodeQ), 0: 128-B float 4-wide nodes
-#endif
-#ifndef RT_FULL_SORT
-#define RT_FULL_SORT 0                   // 4-wide: 1 = 5-comparator near-first sort; 0 = 3-comparator tournament (C3 +1.2 %)
-#endif
-#ifndef RT_BVH_WIDTH
-#define RT_BVH_WIDTH 4                   // children per node: 4 (64-B nodes) or 8 (96-B nodes; C3 4045 vs 4596 Mrays/s)
-#endif
-static_assert(RT_BVH_WIDTH == 4 || (RT_BVH_WIDTH == 8 && RT_QNODE), "8-wide nodes are quantised only");
-[[maybe_unused]] constexpr int kNodeF4 = RT_QNODE ? (RT_BVH_WIDTH == 8 ? 6 : 4) : 8;   // float4 per node
+constexpr int kNodeF4 = 4;                       // float4 per quantised 4-wide node (rt_bvh.h Node4Q)
 constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
     return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
 }
 
-__device__ __forceinline__ void slab(float lx, float ly, float lz, float hx, float hy, float hz, float ix, float iy,
-                                     float iz, float ox, float oy, float oz, float tlo, float thi, float &tn, float &tf) {
-    float t0x = fmaf(lx, ix, -ox), t1x = fmaf(hx, ix, -ox);
-    float t0y = fmaf(ly, iy, -oy), t1y = fmaf(hy, iy, -oy);
-    float t0z = fmaf(lz, iz, -oz), t1z = fmaf(hz, iz, -oz);
-    tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tlo));
-    tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
-}
-
 // One leaf's primitives against q: faces (5 words each) then spheres (2 words),
-// rt_bvh.h leaf_records.  Closest: running (best, win); shadow: valid hits go
-// to the lane's LDS key list (opaque -> early out, > kHits -> brute force).
-__device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, int *hits, Counters &cnt,
-                                           float &best, int &win, int &nh, bool &opaque) {
+// rt_bvh.h leaf_records.  Closest: running (best, win); shadow: every valid
+// hit multiplies the mask (an opaque one ends the ray).
+__device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, Counters &cnt, float &best, int &win,
+                                           bool &opaque) {
     int v = -link - 1;
     const float4 *R = p.leafrec + (v >> 8);
     int nfc = (v >> 4) & 15, count = v & 15;
@@ -379,24 +355,15 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
             } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
                 if (fac == 0.0f && p.shadow_early_out) {
                     opaque = true;
-#if RT_ORDERED_SHADOW
-                } else if (nh < kHits) {
-                    hits[nh * kBlock] = key;
-                    nh++;
-                } else {
-                    q.bf = true;                   // too many: let the scan redo it in order
-#else
                 } else {
                     q.mask = cmulf(q.mask, fac);
-#endif
                 }
             }
         }
     }
 }
 
-// stk: this lane's stack (entries kBlock apart); hits: its kHits-entry list of
-// shadow-hit object keys (also kBlock apart), both in LDS.
+// stk: this lane's traversal stack in LDS (entries kBlock apart).
 //
 // While-while traversal with speculative leaf postponement (Aila & Laine
 // 2009): a lane that reaches a leaf parks it and keeps descending inner nodes
@@ -404,7 +371,7 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 // visited together.  Node visits stay one dependent fetch each, and the leaf
 // code runs with most lanes active instead of in almost every wave trip (+6 %
 // over an if-if loop).  The result does not depend on the visiting order.
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counters &cnt) {
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
     // |1/d| capped at 2^100 (1/0 -> 1e30 as before): the quantised planes'
     // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
     // and the cap is conservative: an axis with |d| < 2^-100 moves the ray by
@@ -412,37 +379,63 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
     const float ix = clampr(safe_rcp(q.d.x), -0x1p100f, 0x1p100f);
     const float iy = clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
     const float iz = clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
-    [[maybe_unused]] const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
+    const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
     const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
     const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
     int win = -1;
-    int nh = 0;
     bool opaque = false;
     // stack entry 0 holds kEmpty for good (written once per kernel): popping
     // the empty stack yields kEmpty with no bounds test
     int sp = 1;
     int node = rtbvh::kEmpty;                  // >= 0 inner node, < 0 leaf, kEmpty: done
     int leaf = rtbvh::kEmpty;                  // postponed leaf
-    // One 4-wide node (rt_bvh.h Node4: lo.x/y/z rows, hi.x/y/z rows, links):
-    // slab-test the children, push the far hits, continue with the nearest,
-    // park the first leaf reached.
-    // children (entry, exit) distances -> push the far hits, continue with the
-    // nearest, park the first leaf reached
-    [[maybe_unused]] auto descend = [&](float n0, float f0, float n1, float f1, float n2, float f2, float n3, float f3, int4 lk) {
+    auto thi_now = [&] {
+        return q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
+    };
+    // One quantised 4-wide node (rt_bvh.h Node4Q): plane a of child i at
+    // origin_a + q * 2^e_a, i.e. t = q * (2^e_a / d_a) + (origin_a - o_a) / d_a
+    // = fma(q, A_a, B_a) -- one fma per plane; the rounding (~ulp(D) in
+    // distance) is far inside the primitive padding.  Slab-test the children,
+    // push the far hits, continue with the nearest, park the first leaf reached.
+    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3) {
 #if RT_PROF
         cnt.trips++;
 #endif
         cnt.boxes += 4;
-        // entry distance of each hit child, +inf for a miss or an empty slot
-        // (unused slots link to the empty leaf, kEmptyLeaf: entering one is
-        // harmless, so no link test; their inverted boxes miss anyway)
-        float k0 = (n0 <= f0) ? n0 : kInf;
-        float k1 = (n1 <= f1) ? n1 : kInf;
-        float k2 = (n2 <= f2) ? n2 : kInf;
-        float k3 = (n3 <= f3) ? n3 : kInf;
-        int c0 = lk.x, c1 = lk.y, c2 = lk.z, c3 = lk.w;
-        // near-first order: 5-comparator sorting network, registers only
+        float thi = thi_now();
+        // 2^e * (1/d): exact power-of-two scaling (one v_bfe_i32 + v_ldexp per
+        // axis; signed exponents in bytes 0..2 of w0.w), finite by the caps
+        const int ex = __float_as_int(w0.w);
+        float Ax = __builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8));
+        float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
+        float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
+        float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
+        unsigned qlx = __float_as_uint(w1.x), qly = __float_as_uint(w1.y), qlz = __float_as_uint(w1.z);
+        unsigned qhx = __float_as_uint(w1.w), qhy = __float_as_uint(w2.x), qhz = __float_as_uint(w2.y);
+        int c0 = __float_as_int(w2.z), c1 = __float_as_int(w2.w), c2 = __float_as_int(w3.x), c3 = __float_as_int(w3.y);
+        // near / far plane per axis by the ray's octant: t(q) = fma(q, A, B) is
+        // monotonic in q with the sign of A (= the sign of 1/d), so
+        // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10
+        const unsigned nx = neg_x ? qhx : qlx, fx = neg_x ? qlx : qhx;
+        const unsigned ny = neg_y ? qhy : qly, fy = neg_y ? qly : qhy;
+        const unsigned nz = neg_z ? qhz : qlz, fz = neg_z ? qlz : qhz;
+        float k[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int sh = 8 * i;
+            float tnx = fmaf((float)((nx >> sh) & 0xffu), Ax, Bx), tfx = fmaf((float)((fx >> sh) & 0xffu), Ax, Bx);
+            float tny = fmaf((float)((ny >> sh) & 0xffu), Ay, By), tfy = fmaf((float)((fy >> sh) & 0xffu), Ay, By);
+            float tnz = fmaf((float)((nz >> sh) & 0xffu), Az, Bz), tfz = fmaf((float)((fz >> sh) & 0xffu), Az, Bz);
+            float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
+            float tf = fminf(fminf(tfx, tfy), fminf(tfz, thi));
+            // entry distance of a hit child, +inf for a miss or an empty slot
+            // (unused slots link to the empty leaf, kEmptyLeaf: entering one is
+            // harmless, so no link test; their inverted boxes miss anyway)
+            k[i] = (tn <= tf) ? tn : kInf;
+        }
+        float k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
+        // nearest child by a 3-comparator tournament, registers only
 #define RT_CSWAP(ka, ca, kb, cb)                 \
     {                                            \
         bool sw = kb < ka;                       \
@@ -456,29 +449,18 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
         RT_CSWAP(k0, c0, k1, c1);
         RT_CSWAP(k2, c2, k3, c3);
         RT_CSWAP(k0, c0, k2, c2);
-#if RT_FULL_SORT
-        RT_CSWAP(k1, c1, k3, c3);
-        RT_CSWAP(k1, c1, k2, c2);
-#endif
 #undef RT_CSWAP
         // branch-free pushes: a missed child is written above the top and not
-        // counted (the LDS stack has one spare entry for it).  Without the full
-        // sort: c0 is the nearest (a tournament), c2 the final's loser goes on
-        // top, the first round's losers c1, c3 below it in either order -- the
-        // visiting order only affects speed, every hit child is visited
+        // counted (the LDS stack has one spare entry for it).  c0 is the
+        // nearest, c2 (the final's loser) goes on top, the first round's
+        // losers c1, c3 below it -- the visiting order only affects speed,
+        // every hit child is visited
         stk[sp * kBlock] = c3;
         sp += k3 < kInf ? 1 : 0;
-#if RT_FULL_SORT
-        stk[sp * kBlock] = c2;
-        sp += k2 < kInf ? 1 : 0;
-        stk[sp * kBlock] = c1;
-        sp += k1 < kInf ? 1 : 0;
-#else
         stk[sp * kBlock] = c1;
         sp += k1 < kInf ? 1 : 0;
         stk[sp * kBlock] = c2;
         sp += k2 < kInf ? 1 : 0;
-#endif
         if (k0 < kInf) {
             node = c0;
         } else {
@@ -489,168 +471,23 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             node = stk[(--sp) * kBlock];
         }
     };
-    auto thi_now = [&] {
-        return q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
-    };
-#if !RT_QNODE
-    // full-precision node (rt_bvh.h Node4)
-    auto visit = [&](float4 lx, float4 ly, float4 lz, float4 hx, float4 hy, float4 hz, int4 lk) {
-        float thi = thi_now();
-        float n0, f0, n1, f1, n2, f2, n3, f3;
-        slab(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, ix, iy, iz, ox, oy, oz, tlo, thi, n0, f0);
-        slab(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, ix, iy, iz, ox, oy, oz, tlo, thi, n1, f1);
-        slab(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, ix, iy, iz, ox, oy, oz, tlo, thi, n2, f2);
-        slab(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, ix, iy, iz, ox, oy, oz, tlo, thi, n3, f3);
-        descend(n0, f0, n1, f1, n2, f2, n3, f3, lk);
-    };
-#elif RT_BVH_WIDTH == 4
-    // quantised node (rt_bvh.h Node4Q): plane a of child i at
-    // origin_a + q * 2^e_a, i.e. t = q * (2^e_a / d_a) + (origin_a - o_a) / d_a
-    // = fma(q, A_a, B_a) -- one fma per plane, like the full-precision slab;
-    // the rounding (~ulp(D) in distance) is far inside the primitive padding.
-    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3) {
-        float thi = thi_now();
-        // 2^e * (1/d): exact power-of-two scaling (one v_bfe_i32 + v_ldexp per
-        // axis; signed exponents in bytes 0..2 of w0.w), finite by the caps
-        const int ex = __float_as_int(w0.w);
-        float Ax = __builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8));
-        float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
-        float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
-        float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
-        unsigned qlx = __float_as_uint(w1.x), qly = __float_as_uint(w1.y), qlz = __float_as_uint(w1.z);
-        unsigned qhx = __float_as_uint(w1.w), qhy = __float_as_uint(w2.x), qhz = __float_as_uint(w2.y);
-        int4 lk = make_int4(__float_as_int(w2.z), __float_as_int(w2.w), __float_as_int(w3.x), __float_as_int(w3.y));
-        // near / far plane per axis by the ray's octant: t(q) = fma(q, A, B) is
-        // monotonic in q with the sign of A (= the sign of 1/d), so
-        // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10
-        const unsigned nx = neg_x ? qhx : qlx, fx = neg_x ? qlx : qhx;
-        const unsigned ny = neg_y ? qhy : qly, fy = neg_y ? qly : qhy;
-        const unsigned nz = neg_z ? qhz : qlz, fz = neg_z ? qlz : qhz;
-        float tn[4], tf[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int sh = 8 * i;
-            float tnx = fmaf((float)((nx >> sh) & 0xffu), Ax, Bx), tfx = fmaf((float)((fx >> sh) & 0xffu), Ax, Bx);
-            float tny = fmaf((float)((ny >> sh) & 0xffu), Ay, By), tfy = fmaf((float)((fy >> sh) & 0xffu), Ay, By);
-            float tnz = fmaf((float)((nz >> sh) & 0xffu), Az, Bz), tfz = fmaf((float)((fz >> sh) & 0xffu), Az, Bz);
-            tn[i] = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
-            tf[i] = fminf(fminf(tfx, tfy), fminf(tfz, thi));
-        }
-        descend(tn[0], tf[0], tn[1], tf[1], tn[2], tf[2], tn[3], tf[3], lk);
-    };
-#else
-    // quantised 8-wide node (rt_bvh.h Node8Q, 6 x 16 B): the same planes, the
-    // children ordered near-first by the 19-comparator sorting network for 8
-    // keys (entry distance, link pairs, registers only)
-    auto visit_q8 = [&](float4 w0, float4 w1, float4 w2, float4 w3, float4 w4, float4 w5) {
-#if RT_PROF
-        cnt.trips++;
-#endif
-        cnt.boxes += 8;
-        float thi = thi_now();
-        const int ex = __float_as_int(w0.w);
-        float Ax = __builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8));
-        float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
-        float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
-        float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
-        const unsigned qlx[2] = {__float_as_uint(w1.x), __float_as_uint(w1.y)};
-        const unsigned qly[2] = {__float_as_uint(w1.z), __float_as_uint(w1.w)};
-        const unsigned qlz[2] = {__float_as_uint(w2.x), __float_as_uint(w2.y)};
-        const unsigned qhx[2] = {__float_as_uint(w2.z), __float_as_uint(w2.w)};
-        const unsigned qhy[2] = {__float_as_uint(w3.x), __float_as_uint(w3.y)};
-        const unsigned qhz[2] = {__float_as_uint(w3.z), __float_as_uint(w3.w)};
-        int c[8] = {__float_as_int(w4.x), __float_as_int(w4.y), __float_as_int(w4.z), __float_as_int(w4.w),
-                    __float_as_int(w5.x), __float_as_int(w5.y), __float_as_int(w5.z), __float_as_int(w5.w)};
-        float k[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int wd = i >> 2, sh = 8 * (i & 3);
-            float t0x = fmaf((float)((qlx[wd] >> sh) & 0xffu), Ax, Bx), t1x = fmaf((float)((qhx[wd] >> sh) & 0xffu), Ax, Bx);
-            float t0y = fmaf((float)((qly[wd] >> sh) & 0xffu), Ay, By), t1y = fmaf((float)((qhy[wd] >> sh) & 0xffu), Ay, By);
-            float t0z = fmaf((float)((qlz[wd] >> sh) & 0xffu), Az, Bz), t1z = fmaf((float)((qhz[wd] >> sh) & 0xffu), Az, Bz);
-            float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tlo));
-            float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), thi));
-            k[i] = ((tn <= tf) & (c[i] != rtbvh::kEmpty)) ? tn : kInf;
-        }
-#define RT_CSWAP8(a, b)                          \
-    {                                            \
-        bool sw = k[b] < k[a];                   \
-        float tk = sw ? k[b] : k[a];             \
-        k[b] = sw ? k[a] : k[b];                 \
-        k[a] = tk;                               \
-        int tc = sw ? c[b] : c[a];               \
-        c[b] = sw ? c[a] : c[b];                 \
-        c[a] = tc;                               \
-    }
-        RT_CSWAP8(0, 2) RT_CSWAP8(1, 3) RT_CSWAP8(4, 6) RT_CSWAP8(5, 7)
-        RT_CSWAP8(0, 4) RT_CSWAP8(1, 5) RT_CSWAP8(2, 6) RT_CSWAP8(3, 7)
-        RT_CSWAP8(0, 1) RT_CSWAP8(2, 3) RT_CSWAP8(4, 5) RT_CSWAP8(6, 7)
-        RT_CSWAP8(2, 4) RT_CSWAP8(3, 5)
-        RT_CSWAP8(1, 4) RT_CSWAP8(3, 6)
-        RT_CSWAP8(1, 2) RT_CSWAP8(3, 4) RT_CSWAP8(5, 6)
-#undef RT_CSWAP8
-#pragma unroll
-        for (int i = 7; i >= 1; i--) {
-            stk[sp * kBlock] = c[i];
-            sp += k[i] < kInf ? 1 : 0;
-        }
-        if (k[0] < kInf) {
-            node = c[0];
-        } else {
-            node = stk[(--sp) * kBlock];
-        }
-        if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
-            leaf = node;                       // park it, keep descending
-            node = stk[(--sp) * kBlock];
-        }
-    };
-#endif
     // The root (every trace starts there; wave-uniform) comes through scalar
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
     // (loads and stores share vmcnt, in order).
-#if RT_QNODE && RT_BVH_WIDTH == 8
-    visit_q8(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4), sld4(p.bvh, 5));
-#elif RT_QNODE
     visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3));
-#else
-    visit(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4), sld4(p.bvh, 5),
-          [&] {
-              float4 l = sld4(p.bvh, 6);
-              return make_int4(__float_as_int(l.x), __float_as_int(l.y), __float_as_int(l.z), __float_as_int(l.w));
-          }());
-#endif
     for (;;) {
         while (node >= 0) {
 #if RT_PROF >= 2
             const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
-#if RT_QNODE
             const float4 *N = p.bvh + kNodeF4 * node;
             float4 w0 = N[0], w1 = N[1], w2 = N[2], w3 = N[3];
-#if RT_BVH_WIDTH == 8
-            float4 w4 = N[4], w5 = N[5];
-#endif
 #if RT_PROF >= 2
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w3.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
-#if RT_BVH_WIDTH == 8
-            visit_q8(w0, w1, w2, w3, w4, w5);
-#else
             visit_q(w0, w1, w2, w3);
-#endif
-#else
-            const float4 *N = p.bvh + 8 * node;
-            float4 lx = N[0], ly = N[1], lz = N[2], hx = N[3], hy = N[4], hz = N[5], lkf = N[6];
-            int4 lk = make_int4(__float_as_int(lkf.x), __float_as_int(lkf.y), __float_as_int(lkf.z),
-                                __float_as_int(lkf.w));
-#if RT_PROF >= 2
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(lkf.w), "v"(lx.x), "v"(hz.w) : "memory");
-            cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
-#endif
-            visit(lx, ly, lz, hx, hy, hz, lk);
-#endif
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
@@ -661,9 +498,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
 #if RT_PROF
             cnt.trips++;
 #endif
-            leaf_visit(q, p, leaf, hits, cnt, best, win, nh, opaque);
+            leaf_visit(q, p, leaf, cnt, best, win, opaque);
             leaf = rtbvh::kEmpty;
-            if (opaque || q.bf) {
+            if (opaque) {
                 node = rtbvh::kEmpty;
                 break;
             }
@@ -679,22 +516,8 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
             q.tmax = best;
             q.win = win;
         }
-    } else if (!q.bf) {
-        if (opaque) {
-            q.mask = {0.0f, 0.0f, 0.0f};
-        } else if (RT_ORDERED_SHADOW) {
-            // multiply in object order (insertion sort of the LDS list; nh <= kHits)
-            for (int i = 1; i < nh; i++) {
-                int k = hits[i * kBlock];
-                int j = i - 1;
-                while (j >= 0 && hits[j * kBlock] > k) {
-                    hits[(j + 1) * kBlock] = hits[j * kBlock];
-                    j--;
-                }
-                hits[(j + 1) * kBlock] = k;
-            }
-            for (int i = 0; i < nh; i++) q.mask = cmulf(q.mask, cst(p.ofac)[hits[i * kBlock]]);
-        }
+    } else if (opaque) {
+        q.mask = {0.0f, 0.0f, 0.0f};
     }
 }
 
@@ -703,74 +526,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, int *hits, Counte
 // ---------------------------------------------------------------------------
 enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4 };
 
-// RT_GLOBAL_FRAMES: the frames live in a device buffer, each lane's MAXF frames
-// contiguous (AoS per lane) -- see LaneState.  RT_FRAME_NT: every frame field
-// is read and written with non-temporal accesses, which bypass the 32 KiB L1
-// (MI355X_MICROARCH.md, L1 bypass): a frame is written at one shade node and
-// read back after a trace, never reused from L1, and streaming it through L1
-// evicted the BVH nodes the next traversal needs.
-#ifndef RT_GLOBAL_FRAMES
-#define RT_GLOBAL_FRAMES 1
-#endif
-// RT_FRAME_NT: 0 plain accesses; 1 non-temporal loads; 2 relaxed agent-scope
-// atomic loads (global_load ... sc1); 3 non-temporal loads and stores (the
-// stores then stream past L2 as well: 2.2x slower, measured).  Stores are
-// plain for 1 and 2.
-#ifndef RT_FRAME_NT
-#define RT_FRAME_NT 0
-#endif
-template <typename T>
-struct NTf {
-    T v;
-    __device__ __forceinline__ operator T() const {
-#if RT_FRAME_NT == 2
-        return __hip_atomic_load(&v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-        return __builtin_nontemporal_load(&v);
-#endif
-    }
-    __device__ __forceinline__ NTf &operator=(T x) {
-#if RT_FRAME_NT == 3
-        __builtin_nontemporal_store(x, &v);
-#else
-        v = x;
-#endif
-        return *this;
-    }
-    __device__ __forceinline__ NTf &operator=(const NTf &o) { return *this = (T)o; }
-    __device__ __forceinline__ T operator++(int) {
-        T t = *this;
-        *this = t + 1;
-        return t;
-    }
-};
-struct NTV3 {
-    NTf<float> x, y, z;
-    __device__ __forceinline__ operator V3() const { return {x, y, z}; }
-    __device__ __forceinline__ NTV3 &operator=(V3 a) {
-        x = a.x, y = a.y, z = a.z;
-        return *this;
-    }
-};
-struct NTC3 {
-    NTf<float> r, g, b;
-    __device__ __forceinline__ operator C3() const { return {r, g, b}; }
-    __device__ __forceinline__ NTC3 &operator=(C3 a) {
-        r = a.r, g = a.g, b = a.b;
-        return *this;
-    }
-};
-#if RT_FRAME_NT
-typedef NTf<int> FInt;
-typedef NTf<float> FFloat;
-typedef NTV3 FV3;
-typedef NTC3 FC3;
-#else
+// The frames live in a device buffer, each lane's MAXF frames contiguous (AoS
+// per lane, one 128-B line each at depth 4) -- see LaneState.
 typedef int FInt;
 typedef float FFloat;
 typedef V3 FV3;
 typedef C3 FC3;
-#endif
 
 // No depth field: frame k of a lane's stack is at recursion depth p.depth - k.
 // At MAXF = 5 (depth 4) a frame is 32 words = one 128-B cache line, and the
@@ -1002,18 +763,14 @@ __device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAX
     c.sn = n;
 }
 
-// Lane state between scans.
-// RT_GLOBAL_FRAMES: compiler scratch interleaves lanes per dword, so a store by
-// the ~30 % of lanes active in a shading branch dirties whole sectors of
-// mostly-unchanged neighbours and the write-back traffic is ~4x the bytes
-// written; per-lane contiguous frames only dirty the lane's own sectors.
+// Lane state between scans.  The frames are in a device buffer, not compiler
+// scratch: scratch interleaves lanes per dword, so a store by the ~30 % of
+// lanes active in a shading branch dirties whole sectors of mostly-unchanged
+// neighbours and the write-back traffic is ~4x the bytes written; per-lane
+// contiguous frames only dirty the lane's own sectors.
 template <int MAXF>
 struct LaneState {
-#if RT_GLOBAL_FRAMES
     Frame<MAXF> *fr;                 // this lane's frames in Params::frames
-#else
-    Frame<MAXF> fr[MAXF];
-#endif
     int top;                         // -1: primary ray pending
 };
 
@@ -1256,13 +1013,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
-#if RT_GLOBAL_FRAMES
     ls.fr = reinterpret_cast<Frame<MAXF> *>(p.frames) + ((size_t)blockIdx.x * kBlock + threadIdx.x) * MAXF;
-#endif
     Counters cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
-    int *hits = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: hits[k * kBlock], k < kHits
-    int *stk = hits + kHits * kBlock;                       //           stack[k * kBlock]
+    int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
     if (MODE == MODE_BVH) stk[0] = rtbvh::kEmpty;           // bvh_trace's stack bottom (never overwritten)
     Query q;
     bool busy = false;         // lane owns a pixel
@@ -1363,7 +1117,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(search && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (search && !q.bf) bvh_trace(q, p, stk, hits, cnt);
+            if (search && !q.bf) bvh_trace(q, p, stk, cnt);
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1441,8 +1195,9 @@ struct RenderSlot {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     unsigned int *work = nullptr;
     unsigned long long *stats = nullptr;
-    void *d_frames = nullptr;          // RT_GLOBAL_FRAMES buffer
+    void *d_frames = nullptr;          // ShadeRay frames of the launch
     size_t frames_cap = 0;
+    bool used = false;                 // ev1 marks a render issued through this slot
 };
 
 struct rt_scene {
@@ -1481,6 +1236,7 @@ struct rt_scene {
     int bvh_depth = 0;
     int bvh_stack = 0;
     bool bvh_ok = false;
+    double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
     long long bvh_nodes = 0;
     bool last_valid = false;
@@ -1508,7 +1264,7 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     if (mode == MODE_SCAN_LDS) return s->lds_bytes;
     if (mode == MODE_BVH)
-        return (size_t)(kHits + s->bvh_stack + 2) * kBlock * sizeof(int);   // + sentinel + spare
+        return (size_t)(s->bvh_stack + 2) * kBlock * sizeof(int);   // + sentinel + spare
     return 0;
 }
 
@@ -1523,7 +1279,6 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
     Params pl = p;
-#if RT_GLOBAL_FRAMES
     size_t fbytes = (size_t)grid * kBlock * MAXF * sizeof(Frame<MAXF>);
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
@@ -1538,7 +1293,6 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
         }
     }
     pl.frames = slot.d_frames;
-#endif
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
     s->last_lds = (long long)shm;
@@ -1574,6 +1328,7 @@ double distance_bound(const rt_scene *s, const float eye[3]) {
 //   face   pad = 2^-16 * D * max(1, cond)                 (32x the rounding bound)
 //   sphere radius' = sqrt(r^2 + 2^-18 D^2) + 2^-16 D     (discriminant error)
 int build_bvh(rt_scene *s, double D) {
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<rtbvh::Prim> P(s->prims.size());
     for (size_t i = 0; i < P.size(); i++) {
         const auto &src = s->prims[i];
@@ -1612,14 +1367,11 @@ int build_bvh(rt_scene *s, double D) {
     B.max_leaf = (int)s->opt_bvh_leaf;
     B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
     bool ok = B.build(R);
-    rtbvh::ResultW<RT_BVH_WIDTH> Q;
+    rtbvh::Result4 Q;
     if (ok && !R.nodes.empty()) {
-        rtbvh::collapse<RT_BVH_WIDTH>(R, Q);
+        rtbvh::collapse<4>(R, Q);
         rtbvh::bfs_order(Q);                 // top levels first (cache locality of the hot nodes)
     }
-    s->bvh_depth = Q.depth;
-    s->bvh_stack = Q.max_stack;
-    s->bvh_nodes = (long long)Q.nodes.size();
     // leaf records: face = its 5 scan words with (key, shadow factor) in the
     // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
     std::vector<float4> rec;
@@ -1640,38 +1392,49 @@ int build_bvh(rt_scene *s, double D) {
             return 2;
         });
     rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
-#if RT_QNODE
-    std::vector<rtbvh::NodeQ<RT_BVH_WIDTH>> QQ;
+    std::vector<rtbvh::Node4Q> QQ;
     if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ)) ok = false;     // non-finite geometry: scan
     for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
         for (auto &l : z.link)
             if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
-    const void *nodes = QQ.data();
-    size_t node_bytes = QQ.size() * sizeof(QQ[0]);
-#else
-    for (auto &z : Q.nodes)
-        for (auto &l : z.link)
-            if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
-    const void *nodes = Q.nodes.data();
-    size_t node_bytes = Q.nodes.size() * sizeof(rtbvh::Node4);
-#endif
     // the device stack holds kStack entries: a deeper tree uses the scan
-    s->bvh_ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
-    s->bvh_D = D;
-    if (!s->bvh_ok) return RT_OK;                              // fall back to the scan
-    if (s->d_bvh) (void)hipFree(s->d_bvh);
-    if (s->d_leafrec) (void)hipFree(s->d_leafrec);
-    s->d_bvh = nullptr;
-    s->d_leafrec = nullptr;
-    if (hipMalloc(&s->d_bvh, node_bytes) != hipSuccess) return RT_E_NOMEM;
-    if (hipMalloc(&s->d_leafrec, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMemcpy(s->d_bvh, nodes, node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-        (!rec.empty() &&
-         hipMemcpy(s->d_leafrec, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess))
-        return RT_E_HIP;
-    s->base.bvh = s->d_bvh;
-    s->base.leafrec = s->d_leafrec;
-    return RT_OK;
+    ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
+    // The old tree stays valid until the new one is on the device: upload into
+    // new buffers first, then swap (a failed rebuild leaves no dangling
+    // pointers and no tree marked valid that is not there).
+    float4 *nb = nullptr, *nr = nullptr;
+    int rc = RT_OK;
+    if (ok) {
+        const size_t node_bytes = QQ.size() * sizeof(QQ[0]);
+        if (hipMalloc(&nb, node_bytes) != hipSuccess ||
+            hipMalloc(&nr, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess)
+            rc = RT_E_NOMEM;
+        else if (hipMemcpy(nb, QQ.data(), node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+                 hipMemcpy(nr, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess)
+            rc = RT_E_HIP;
+        if (rc) {
+            if (nb) (void)hipFree(nb);
+            if (nr) (void)hipFree(nr);
+            nb = nr = nullptr;
+        }
+    }
+    // renders still queued may read the old tree: free it after they finish
+    if (s->d_bvh || s->d_leafrec) {
+        (void)hipDeviceSynchronize();
+        if (s->d_bvh) (void)hipFree(s->d_bvh);
+        if (s->d_leafrec) (void)hipFree(s->d_leafrec);
+    }
+    s->d_bvh = nb;
+    s->d_leafrec = nr;
+    s->base.bvh = nb;
+    s->base.leafrec = nr;
+    s->bvh_ok = ok && rc == RT_OK;
+    s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
+    s->bvh_depth = s->bvh_ok ? Q.depth : 0;
+    s->bvh_stack = s->bvh_ok ? Q.max_stack : 0;
+    s->bvh_nodes = s->bvh_ok ? (long long)Q.nodes.size() : 0;
+    s->bvh_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
 }
 
 int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = false) {
@@ -2002,6 +1765,11 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
         if (hipEventRecord(slot.ev_in, caller) != hipSuccess) return RT_E_HIP;
         if (hipStreamWaitEvent(slot.stream, slot.ev_in, 0) != hipSuccess) return RT_E_HIP;
         st = slot.stream;
+    } else if (slot.used && hipStreamWaitEvent(st, slot.ev1, 0) != hipSuccess) {
+        // one slot, any caller stream: this render reuses the slot's work
+        // counter, counters and frames, so it waits for the slot's previous
+        // render (issued on whatever stream) before touching them
+        return RT_E_HIP;
     }
     p.work = slot.work;
     p.stats = slot.stats;
@@ -2012,6 +1780,7 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
     (void)hipEventRecord(slot.ev0, st);
     int rc = launch(s, slot, p, st);
     (void)hipEventRecord(slot.ev1, st);
+    slot.used = true;
     if (slot.stream && hipStreamWaitEvent(caller, slot.ev1, 0) != hipSuccess) return RT_E_HIP;
     s->last_valid = rc == RT_OK;
     return rc;

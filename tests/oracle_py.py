@@ -30,6 +30,8 @@ def lib() -> C.CDLL:
         L.oracle_set_depth.argtypes = [C.c_void_p, C.c_int]
         L.oracle_render_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
                                          C.c_void_p, C.c_void_p]
+        L.oracle_render_pixels.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                           C.c_void_p, C.c_void_p]
         L.oracle_write_ppm.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int]
         L.oracle_quantize.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
         L.oracle_counts_objects.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -118,6 +120,16 @@ class OracleScene:
         cnt = np.zeros(6, dtype=np.int64)
         lib().oracle_render_rows(self._h, W, H, rows.ctypes.data, len(rows), threads, out.ctypes.data,
                                  cnt.ctypes.data)
+        names = ["primary", "shadow", "refraction", "reflection", "skip_trans", "ub_back"]
+        return out, dict(zip(names, (int(c) for c in cnt)))
+
+    def render_pixels(self, W: int, H: int, xy, threads: int = 0):
+        """Pixels (x, y) of the W x H image -> (float32 [n, 3], counts dict)."""
+        xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
+        out = np.empty((len(xy), 3), dtype=np.float32)
+        cnt = np.zeros(6, dtype=np.int64)
+        lib().oracle_render_pixels(self._h, W, H, xy.ctypes.data, len(xy), threads, out.ctypes.data,
+                                   cnt.ctypes.data)
         names = ["primary", "shadow", "refraction", "reflection", "skip_trans", "ub_back"]
         return out, dict(zip(names, (int(c) for c in cnt)))
 
