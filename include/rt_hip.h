@@ -126,6 +126,11 @@ typedef struct {
     unsigned long long box_tests;    /* ray-box tests executed (BVH traversal) */
     unsigned long long face_tests;   /* ray-triangle tests executed */
     unsigned long long sphere_tests; /* ray-sphere tests executed */
+    unsigned long long shadow_known; /* shadow rays counted above whose cumulative mask was already 0:
+                                        their result is known, they are not searched */
+    unsigned long long bf_queries;   /* queries answered by the brute-force scan (BVH mode fallbacks) */
+    unsigned long long stack_spills; /* BVH traversal stack blocks spilled from LDS to device memory */
+    double bvh_build_ms;             /* host time of the scene's last BVH (re)build (0: none) */
 } rt_stats;
 
 typedef struct rt_scene rt_scene;
@@ -177,7 +182,9 @@ int rt_render_row_blocks(rt_scene *scene, const rt_camera *cam, int W, int H, in
  * With n > 1 each render gets its own work counter, counters and ShadeRay
  * frame buffer and runs on a library stream, ordered against its caller's
  * stream by events: renders issued on different caller streams -- independent
- * frames -- overlap, so one frame's tail is filled by the next frame's work). */
+ * frames -- overlap, so one frame's tail is filled by the next frame's work),
+ * "lds_stack" (12..16, default 14: BVH stack entries kept in LDS per lane;
+ * deeper stacks spill to device memory -- a test knob). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
 /* Raw counters of the last render (diagnostics): [0..8] as in rt_stats,
@@ -187,7 +194,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * [20] BVH nodes, [21] BVH depth, [22] BVH worst-case stack, [23] CUs;
  * launch timeline (100 MHz ticks): [24] first wave start, [26] last wave end;
  * RT_PROF builds also [25] work counter drained, [27] sum of per-wave tails, [28] sum of wave
- * lifetimes, [29] waves.  n <= 32. */
+ * lifetimes, [29] waves; [32] known-zero shadow rays, [33] brute-force queries, [34] stack
+ * spills (as in rt_stats).  n <= 40. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

@@ -294,7 +294,8 @@ inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace
             });
             int nfaces = 0;
             for (int32_t k : ks) nfaces += is_face(k) ? 1 : 0;
-            if (words >= (size_t(1) << 23)) return false;
+            // off <= 2^23 - 2 keeps every link above INT_MIN + 256 (device sentinels)
+            if (words >= (size_t(1) << 23) - 1) return false;
             n.link[i] = -(1 + (int32_t)((words << 8) | (size_t)(nfaces << 4) | (size_t)count));
             for (int32_t k : ks) words += (size_t)emit(k);
         }

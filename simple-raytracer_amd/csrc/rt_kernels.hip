@@ -149,8 +149,10 @@ struct Params {
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
     int dir_bf;                          // directional shadow rays must scan spheres brute force
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
-    int bvh_stack;                       // BVH: LDS stack entries per lane (worst case of the tree)
-    void *__restrict__ frames;           // grid x kBlock x MAXF ShadeRay frames
+    int bvh_stack;                       // BVH: worst-case traversal stack entries of the tree
+    int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
+    void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
+    int *__restrict__ ovf;               // grid x kBlock x kStack spilled BVH stack entries
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -160,7 +162,14 @@ enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif
-constexpr int kStack = 40;               // max per-lane BVH stack entries; LDS holds the tree's bound
+constexpr int kStack = 40;               // max per-lane BVH stack entries (deeper trees: the scan)
+// BVH traversal stack entries per lane in LDS (entry 0: the sentinel); a
+// deeper stack spills its oldest kSpill entries to device memory (rare)
+constexpr int kLdsStack = 16;            // most entries the LDS share may hold (option lds_stack)
+constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading state): 5 blocks per CU
+                                         // on paper, -8.6 % measured; 14: 270 spills per C3 frame
+constexpr int kSpill = 8;
+static_assert(kStack % kSpill == 0 && kLdsStack - 3 > kSpill, "stack spill blocks");
 constexpr int kBlock = 256;
 
 // ---------------------------------------------------------------------------
@@ -302,7 +311,8 @@ struct Counters {
 enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
 constexpr int kNodeF4 = 4;                       // float4 per quantised 4-wide node (rt_bvh.h Node4Q)
-constexpr int kNStats = 32;                      // device counter slots (rt_scene_debug_counters)
+constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
+constexpr int kNStats = 40;                      // device counter slots (rt_scene_debug_counters)
 
 __device__ __forceinline__ float safe_rcp(float x) {
     return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
@@ -393,6 +403,33 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
     auto thi_now = [&] {
         return q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
     };
+    // LDS holds stack entries [0, kLdsStack); entry 0 is kEmpty, or kRefill + b
+    // when b blocks of kSpill older entries wait in device memory (ovf).
+    auto ovf_lane = [&]() -> int * {
+        return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * kStack;
+    };
+    auto spill = [&]() {                       // move the oldest kSpill entries out
+        const int tag = stk[0];
+        const int nb = tag == rtbvh::kEmpty ? 0 : tag - kRefill;
+        int *o = ovf_lane() + nb * kSpill;
+        for (int i = 0; i < kSpill; i++) o[i] = stk[(1 + i) * kBlock];
+        for (int i = kSpill + 1; i < sp; i++) stk[(i - kSpill) * kBlock] = stk[i * kBlock];
+        sp -= kSpill;
+        stk[0] = kRefill + nb + 1;
+        atomicAdd(&p.stats[34], 1ull);
+    };
+    auto pop = [&]() -> int {
+        int n = stk[(--sp) * kBlock];
+        if ((unsigned)n - (unsigned)kRefill - 1u < (unsigned)(kStack / kSpill)) {   // rare: bring a block back
+            const int nb = n - kRefill;
+            const int *o = ovf_lane() + (nb - 1) * kSpill;
+            for (int i = 0; i < kSpill; i++) stk[(1 + i) * kBlock] = o[i];
+            stk[0] = nb > 1 ? n - 1 : rtbvh::kEmpty;
+            sp = kSpill;
+            n = o[kSpill - 1];                 // the block's newest entry is the top
+        }
+        return n;
+    };
     // One quantised 4-wide node (rt_bvh.h Node4Q): plane a of child i at
     // origin_a + q * 2^e_a, i.e. t = q * (2^e_a / d_a) + (origin_a - o_a) / d_a
     // = fma(q, A_a, B_a) -- one fma per plane; the rounding (~ulp(D) in
@@ -434,6 +471,8 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
             // harmless, so no link test; their inverted boxes miss anyway)
             k[i] = (tn <= tf) ? tn : kInf;
         }
+        // up to 3 pushes below write stk[sp .. sp + 2]: make room (rare)
+        if (sp > p.stack_cap - 3) spill();
         float k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
         // nearest child by a 3-comparator tournament, registers only
 #define RT_CSWAP(ka, ca, kb, cb)                 \
@@ -464,11 +503,11 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
         if (k0 < kInf) {
             node = c0;
         } else {
-            node = stk[(--sp) * kBlock];
+            node = pop();
         }
         if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
             leaf = node;                       // park it, keep descending
-            node = stk[(--sp) * kBlock];
+            node = pop();
         }
     };
     // The root (every trace starts there; wave-uniform) comes through scalar
@@ -502,11 +541,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
             leaf = rtbvh::kEmpty;
             if (opaque) {
                 node = rtbvh::kEmpty;
+                stk[0] = rtbvh::kEmpty;        // drop any spilled entries with the rest
                 break;
             }
             if (node < 0 && node != rtbvh::kEmpty) {
                 leaf = node;
-                node = stk[(--sp) * kBlock];
+                node = pop();
             }
         }
         if (node == rtbvh::kEmpty) break;
@@ -526,30 +566,122 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
 // ---------------------------------------------------------------------------
 enum Phase { PH_LIGHT = 0, PH_REFR = 1, PH_REFL = 2, PH_REFR_CHILD = 3, PH_REFL_CHILD = 4 };
 
-// The frames live in a device buffer, each lane's MAXF frames contiguous (AoS
-// per lane, one 128-B line each at depth 4) -- see LaneState.
-typedef int FInt;
-typedef float FFloat;
-typedef V3 FV3;
-typedef C3 FC3;
-
-// No depth field: frame k of a lane's stack is at recursion depth p.depth - k.
-// At MAXF = 5 (depth 4) a frame is 32 words = one 128-B cache line, and the
-// lane's frames are line-aligned (the buffer is, and 5 x 128 B per lane).
-template <int MAXF>
-struct Frame {
-    FInt obj, state, phase, light, sn;
-    FInt stack[MAXF];                // medium stack (incident_object_stack), object indices
-    FFloat ei, et;                   // incidence / transmission refraction index
-    FV3 P, N, I;                     // hit point, shading normal (flipped for spheres), I = -ray
-    FFloat cosI;
-    FC3 dif, acc;                    // diffuse, running colour
-    FFloat Ft;                       // transmission Fresnel F (main.cpp:966)
-    // No shadow mask: it starts at {1,1,1} before the light loop (main.cpp:788)
-    // and lives in the shadow query from one light to the next.
-    FInt pad_[MAXF == 5 ? 3 : 1];    // depth 4: the frame is one 128-B line
+// ShadeRay state of a lane.  The reference recurses (ShadeRay calls itself,
+// main.cpp:1072-1083, :1184-1194); here every lane walks its pixel's shade
+// tree as a state machine with one frame per recursion level.
+//
+//  * LDS, per lane (16 words, kBlock apart: conflict-free): the state of the
+//    node being shaded -- shading normal N (flipped for spheres), I = -ray,
+//    diffuse colour (after the light loop: F_t, the transmission Fresnel,
+//    in its first word), running colour, object, packed phase / light /
+//    medium state / stack size, eta_i, eta_t.  Shading a node, and every
+//    shadow step of it (63 % of the rays), touches no device memory.
+//  * Cold frame per level, in a device buffer (per lane contiguous; not
+//    compiler scratch, which interleaves lanes per dword): the node's medium
+//    stack (written by the transition that opens the node) and -- only when
+//    the node opens a child -- its LDS state and hit point, saved for the
+//    child's return.
+//
+// cos(theta_i) is not stored: it is N.I with the node's final N (main.cpp:
+// 864-872 recompute it after the flip).  The shadow mask is not stored
+// either: it starts at {1,1,1} before the light loop (main.cpp:788) and lives
+// in the shadow query from one light to the next; the hit point of the top
+// node lives in the query's origin.
+enum { PH_DONE = PH_REFL_CHILD + 1 };
+struct HotR {                        // register form of the top node's state
+    V3 N, I;
+    C3 dif;                          // dif.r holds F_t after the light loop
+    C3 acc;
+    int obj;
+    unsigned meta;                   // phase:3 | state:1 | stack size:5 | light:23
+    float ei, et;
 };
+__device__ __forceinline__ int h_phase(const HotR &h) { return (int)(h.meta & 7u); }
+__device__ __forceinline__ int h_state(const HotR &h) { return (int)((h.meta >> 3) & 1u); }
+__device__ __forceinline__ int h_sn(const HotR &h) { return (int)((h.meta >> 4) & 31u); }
+__device__ __forceinline__ int h_light(const HotR &h) { return (int)(h.meta >> 9); }
+__device__ __forceinline__ unsigned mk_meta(int phase, int state, int sn, int light) {
+    return (unsigned)phase | ((unsigned)state << 3) | ((unsigned)sn << 4) | ((unsigned)light << 9);
+}
+__device__ __forceinline__ void set_phase(HotR &h, int phase) { h.meta = (h.meta & ~7u) | (unsigned)phase; }
+__device__ __forceinline__ float cos_i(const HotR &h) { return vdot(h.N, h.I); }
 
+// LDS words of the state (word w of lane l at [w * kBlock + l])
+enum {
+    LW_N = 0, LW_I = 3, LW_DIF = 6, LW_ACC = 9, LW_OBJ = 12, LW_META = 13, LW_EI = 14, LW_ET = 15,
+    kLdsHot = 16
+};
+extern __shared__ float4 rt_lds[];   // dynamic LDS of render_kernel: state, then stack / primitives
+
+__device__ __forceinline__ float *lane_lds() { return reinterpret_cast<float *>(rt_lds) + threadIdx.x; }
+__device__ __forceinline__ void lds_load(HotR &h) {
+    const float *l = lane_lds();
+    h.N = {l[(LW_N + 0) * kBlock], l[(LW_N + 1) * kBlock], l[(LW_N + 2) * kBlock]};
+    h.I = {l[(LW_I + 0) * kBlock], l[(LW_I + 1) * kBlock], l[(LW_I + 2) * kBlock]};
+    h.dif = {l[(LW_DIF + 0) * kBlock], l[(LW_DIF + 1) * kBlock], l[(LW_DIF + 2) * kBlock]};
+    h.acc = {l[(LW_ACC + 0) * kBlock], l[(LW_ACC + 1) * kBlock], l[(LW_ACC + 2) * kBlock]};
+    h.obj = __float_as_int(l[LW_OBJ * kBlock]);
+    h.meta = __float_as_uint(l[LW_META * kBlock]);
+    h.ei = l[LW_EI * kBlock];
+    h.et = l[LW_ET * kBlock];
+}
+__device__ __forceinline__ void lds_store(const HotR &h) {
+    float *l = lane_lds();
+    l[(LW_N + 0) * kBlock] = h.N.x, l[(LW_N + 1) * kBlock] = h.N.y, l[(LW_N + 2) * kBlock] = h.N.z;
+    l[(LW_I + 0) * kBlock] = h.I.x, l[(LW_I + 1) * kBlock] = h.I.y, l[(LW_I + 2) * kBlock] = h.I.z;
+    l[(LW_DIF + 0) * kBlock] = h.dif.r, l[(LW_DIF + 1) * kBlock] = h.dif.g, l[(LW_DIF + 2) * kBlock] = h.dif.b;
+    l[(LW_ACC + 0) * kBlock] = h.acc.r, l[(LW_ACC + 1) * kBlock] = h.acc.g, l[(LW_ACC + 2) * kBlock] = h.acc.b;
+    l[LW_OBJ * kBlock] = __int_as_float(h.obj);
+    l[LW_META * kBlock] = __uint_as_float(h.meta);
+    l[LW_EI * kBlock] = h.ei;
+    l[LW_ET * kBlock] = h.et;
+}
+// what a shadow step changes: the running colour and the light index
+__device__ __forceinline__ void lds_store_light(const HotR &h) {
+    float *l = lane_lds();
+    l[(LW_ACC + 0) * kBlock] = h.acc.r, l[(LW_ACC + 1) * kBlock] = h.acc.g, l[(LW_ACC + 2) * kBlock] = h.acc.b;
+    l[LW_META * kBlock] = __uint_as_float(h.meta);
+}
+// what the light loop's end / a traced refraction or reflection changes
+__device__ __forceinline__ void lds_store_phase(const HotR &h) {
+    float *l = lane_lds();
+    l[LW_DIF * kBlock] = h.dif.r;
+    l[(LW_ACC + 0) * kBlock] = h.acc.r, l[(LW_ACC + 1) * kBlock] = h.acc.g, l[(LW_ACC + 2) * kBlock] = h.acc.b;
+    l[LW_META * kBlock] = __uint_as_float(h.meta);
+}
+
+template <int MAXF>
+struct Cold {
+    float4 saved[4];                 // the node's LDS state while a child runs
+    float P[3];                      // its hit point (incidence_object_intersection.point)
+    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
+    int pad_[(MAXF + 3 + 15) / 16 * 16 - (MAXF + 3)];
+};
+static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17>) == 192, "cold frame sizes");
+
+template <int MAXF>
+__device__ __forceinline__ void cold_save(Cold<MAXF> &c, V3 P, const HotR &h) {
+    f4v *v = reinterpret_cast<f4v *>(c.saved);
+    v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
+    v[1] = f4v{h.I.y, h.I.z, h.dif.r, h.dif.g};
+    v[2] = f4v{h.dif.b, h.acc.r, h.acc.g, h.acc.b};
+    v[3] = f4v{__int_as_float(h.obj), __uint_as_float(h.meta), h.ei, h.et};
+    c.P[0] = P.x, c.P[1] = P.y, c.P[2] = P.z;
+}
+template <int MAXF>
+__device__ __forceinline__ V3 cold_restore(const Cold<MAXF> &c, HotR &h) {
+    const f4v *v = reinterpret_cast<const f4v *>(c.saved);
+    f4v a = v[0], b = v[1], d = v[2], e = v[3];
+    h.N = {a.x, a.y, a.z};
+    h.I = {a.w, b.x, b.y};
+    h.dif = {b.z, b.w, d.x};
+    h.acc = {d.y, d.z, d.w};
+    h.obj = __float_as_int(e.x);
+    h.meta = __float_as_uint(e.y);
+    h.ei = e.z;
+    h.et = e.w;
+    return V3{c.P[0], c.P[1], c.P[2]};
+}
 
 // Hit record of the winning intersection, recomputed exactly as TraceRay did.
 __device__ void hit_geometry(const Params &p, int obj, V3 o, V3 d, float t, V3 &P, V3 &N, V3 &bary) {
@@ -585,56 +717,12 @@ __device__ __forceinline__ float texel(const Params &p, const TexK &t, int x, in
     return (v - 0.0f) * (1.0f - 0.0f) / (255.0f - 0.0f) + 0.0f;   // map(v, 0, 255, 0, 1)
 }
 
-// ShadeRay prologue (main.cpp:785-872): diffuse / texture and the sphere
-// normal flip.  Leaves the frame ready for the light loop.
-static_assert(sizeof(Frame<5>) == 128, "a depth-4 frame is one cache line");
-
-template <int MAXF>
-__device__ void node_begin(const Params &p, Frame<MAXF> &f, V3 o, V3 d, float t) {
-    V3 P, N, bary;
-    hit_geometry(p, f.obj, o, d, t, P, N, bary);
-    const ObjK &ob = p.objs[f.obj];
-    V3 I = vmul(d, -1.0f);
-    float cosI = vdot(N, I);
-    C3 dif = {ob.dif[0], ob.dif[1], ob.dif[2]};
-    if (ob.tex >= 0) {
-        TexK tx = p.texs[ob.tex];
-        float width = (float)tx.w, height = (float)tx.h;
-        if (ob.is_sphere) {                                          // main.cpp:805-826
-            float v = (float)(acos((double)N.z) / kPi);
-            float phi = (float)atan2((double)N.y, (double)N.x);
-            float u = (phi - (float)-kPi) * (1.0f - 0.0f) / ((float)kPi - (float)-kPi) + 0.0f;
-            v = clampr(v, 0.0f, 1.0f);
-            u = clampr(u, 0.0f, 1.0f);
-            int i = (int)clampr((float)round(((double)height - 1.0) * (double)v), 0.0f,
-                                (float)((double)height - 1.0));
-            int j = (int)clampr((float)round(((double)width - 1.0) * (double)u), 0.0f,
-                                (float)((double)width - 1.0));
-            dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
-        } else {                                                     // main.cpp:834-861
-            const FaceShadeK &fs = p.fsh[f.obj];
-            float u = (bary.x * fs.vt[0][0]) + (bary.y * fs.vt[1][0]) + (bary.z * fs.vt[2][0]);
-            float v = (bary.x * fs.vt[0][1]) + (bary.y * fs.vt[1][1]) + (bary.z * fs.vt[2][1]);
-            v = clampr(v, 0.0f, 1.0f);
-            u = clampr(u, 0.0f, 1.0f);
-            int i = (int)clampr(roundf((width - 1.0f) * u), 0.0f, (float)((double)width - 1.0));
-            int j = (int)clampr(roundf((height - 1.0f) * v), 0.0f, (float)((double)height - 1.0));
-            dif = {texel(p, tx, i, j, 0), texel(p, tx, i, j, 1), texel(p, tx, i, j, 2)};
-        }
-    }
-    if ((double)cosI < 0.0 && ob.is_sphere) {                      // main.cpp:869-872
-        N = vmul(N, -1.0f);
-        cosI = vdot(N, I);
-    }
-    f.P = P;
-    f.N = N;
-    f.I = I;
-    f.cosI = cosI;
-    f.dif = dif;
-    f.acc = C3{0.0f, 0.0f, 0.0f};    // tmp_specular while lights run
-    f.light = 0;
-    f.phase = PH_LIGHT;
-}
+// ShadeRay prologue (main.cpp:785-872): hit record, diffuse / texture and the
+// sphere normal flip, for the node opened on object `obj` by the closest hit
+// at t along (o, d) with medium state m.  Writes the node's LDS state, ready
+// for the light loop; returns the hit point.
+struct Medium;
+__device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m);
 
 // Direction of light l's shadow ray and the L vector (main.cpp:885-928).
 __device__ __forceinline__ void light_vectors(const LightK &lt, V3 P, V3 &L, V3 &sdir, float &distL, bool &unb) {
@@ -673,312 +761,358 @@ __device__ __forceinline__ float schlick(float F0, float cosI) {
     float p5 = (x2 * x2) * x;
     return (float)((double)F0 + (1.0 - (double)F0) * (double)p5);
 }
+// reflection Fresnel of object ob at cos(theta_i) (main.cpp:1103-1104)
+__device__ __forceinline__ float refl_fresnel(const ObjK &ob, float cosI) {
+    float F0 = (ob.eta - 1) / (ob.eta + 1);
+    return schlick(F0 * F0, cosI);
+}
 
 template <int MAXF>
-__device__ __forceinline__ bool in_stack(const Frame<MAXF> &f, int obj) {
+__device__ __forceinline__ bool in_stack(const Cold<MAXF> &f, int sn, int obj) {
     bool in = false;
-    for (int q = 0; q < f.sn; q++) in |= (f.stack[q] == obj);
+    for (int q = 0; q < sn; q++) in |= (f.stack[q] == obj);
     return in;
+}
+
+// The child's medium state after a transition: state, stack size, eta_i, eta_t
+// (its stack is written into the child's cold frame).
+struct Medium {
+    int state, sn;
+    float ei, et;
+};
+
+__device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m) {
+    V3 P, N, bary;
+    hit_geometry(p, obj, o, d, t, P, N, bary);
+    const ObjK &ob = p.objs[obj];
+    V3 I = vmul(d, -1.0f);
+    float cosI = vdot(N, I);
+    C3 dif = {ob.dif[0], ob.dif[1], ob.dif[2]};
+    if (ob.tex >= 0) {
+        TexK tx = p.texs[ob.tex];
+        float width = (float)tx.w, height = (float)tx.h;
+        if (ob.is_sphere) {                                          // main.cpp:805-826
+            float v = (float)(acos((double)N.z) / kPi);
+            float phi = (float)atan2((double)N.y, (double)N.x);
+            float u = (phi - (float)-kPi) * (1.0f - 0.0f) / ((float)kPi - (float)-kPi) + 0.0f;
+            v = clampr(v, 0.0f, 1.0f);
+            u = clampr(u, 0.0f, 1.0f);
+            int i = (int)clampr((float)round(((double)height - 1.0) * (double)v), 0.0f,
+                                (float)((double)height - 1.0));
+            int j = (int)clampr((float)round(((double)width - 1.0) * (double)u), 0.0f,
+                                (float)((double)width - 1.0));
+            dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
+        } else {                                                     // main.cpp:834-861
+            const FaceShadeK &fs = p.fsh[obj];
+            float u = (bary.x * fs.vt[0][0]) + (bary.y * fs.vt[1][0]) + (bary.z * fs.vt[2][0]);
+            float v = (bary.x * fs.vt[0][1]) + (bary.y * fs.vt[1][1]) + (bary.z * fs.vt[2][1]);
+            v = clampr(v, 0.0f, 1.0f);
+            u = clampr(u, 0.0f, 1.0f);
+            int i = (int)clampr(roundf((width - 1.0f) * u), 0.0f, (float)((double)width - 1.0));
+            int j = (int)clampr(roundf((height - 1.0f) * v), 0.0f, (float)((double)height - 1.0));
+            dif = {texel(p, tx, i, j, 0), texel(p, tx, i, j, 1), texel(p, tx, i, j, 2)};
+        }
+    }
+    if ((double)cosI < 0.0 && ob.is_sphere) {                      // main.cpp:869-872
+        N = vmul(N, -1.0f);
+    }
+    HotR h;
+    h.N = N;
+    h.I = I;
+    h.dif = dif;
+    h.acc = C3{0.0f, 0.0f, 0.0f};    // tmp_specular while lights run
+    h.obj = obj;
+    h.meta = mk_meta(PH_LIGHT, m.state, m.sn, 0);
+    h.ei = m.ei;
+    h.et = m.et;
+    lds_store(h);
+    return P;
 }
 
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
 template <int MAXF>
-__device__ void refr_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit, Counters &cnt) {
-    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
-    int n = f.sn;
+__device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
+                                  Counters &cnt) {
+    const int fsn = h_sn(f);
+    for (int q = 0; q < fsn; q++) c.stack[q] = fc.stack[q];
+    int n = fsn;
+    Medium m;
     float hit_eta = p.objs[hit].eta;
-    if (f.state == ENTERING) {
+    if (h_state(f) == ENTERING) {
         if (hit == f.obj) {
-            c.state = EXITING;
+            m.state = EXITING;
             if (n > 0) {
-                c.ei = p.objs[c.stack[n - 1]].eta;
+                m.ei = p.objs[c.stack[n - 1]].eta;
                 n--;
             } else {
-                c.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
+                m.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
                 cnt.ub++;
             }
-            c.et = n > 0 ? p.objs[c.stack[n - 1]].eta : p.eta_bkg;
+            m.et = n > 0 ? p.objs[c.stack[n - 1]].eta : p.eta_bkg;
             if (n > 0) n--;
         } else {
-            c.state = ENTERING;
-            c.ei = f.et;
-            c.et = hit_eta;
+            m.state = ENTERING;
+            m.ei = f.et;
+            m.et = hit_eta;
             c.stack[n++] = hit;
         }
     } else if (n > 0) {
-        if (!in_stack(f, hit)) {
-            c.state = ENTERING;
-            c.ei = f.et;
-            c.et = hit_eta;
+        if (!in_stack(fc, fsn, hit)) {
+            m.state = ENTERING;
+            m.ei = f.et;
+            m.et = hit_eta;
             c.stack[n++] = hit;
         } else {
-            c.state = EXITING;
-            c.ei = f.et;
-            c.et = p.objs[c.stack[n - 1]].eta;
+            m.state = EXITING;
+            m.ei = f.et;
+            m.et = p.objs[c.stack[n - 1]].eta;
             n--;
         }
     } else {
-        c.state = ENTERING;
-        c.ei = p.eta_bkg;
-        c.et = hit_eta;
+        m.state = ENTERING;
+        m.ei = p.eta_bkg;
+        m.et = hit_eta;
         c.stack[0] = hit;
         n = 1;
     }
-    c.sn = n;
+    m.sn = n;
+    return m;
 }
 
 // Medium-stack transition for the reflection child (main.cpp:1134-1182).
 template <int MAXF>
-__device__ void refl_transition(const Params &p, const Frame<MAXF> &f, Frame<MAXF> &c, int hit) {
-    for (int q = 0; q < f.sn; q++) c.stack[q] = f.stack[q];
-    int n = f.sn;
+__device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit) {
+    const int fsn = h_sn(f);
+    for (int q = 0; q < fsn; q++) c.stack[q] = fc.stack[q];
+    int n = fsn;
+    Medium m;
     float hit_eta = p.objs[hit].eta;
-    if (f.state == ENTERING) {
-        c.state = ENTERING;
-        c.ei = f.ei;
+    if (h_state(f) == ENTERING) {
+        m.state = ENTERING;
+        m.ei = f.ei;
         if (n > 0) {
-            if (!in_stack(f, hit)) {
-                c.et = hit_eta;
+            if (!in_stack(fc, fsn, hit)) {
+                m.et = hit_eta;
                 c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
             } else {
-                c.et = p.objs[c.stack[n - 1]].eta;
+                m.et = p.objs[c.stack[n - 1]].eta;
                 n--;
             }
         } else {
-            c.et = hit_eta;
+            m.et = hit_eta;
             c.stack[0] = hit;
             n = 1;
         }
     } else {
-        c.ei = f.ei;
+        m.ei = f.ei;
         if (hit == f.obj) {
-            c.state = EXITING;
-            c.et = f.et;
+            m.state = EXITING;
+            m.et = f.et;
         } else {
-            c.state = ENTERING;
-            c.et = hit_eta;
+            m.state = ENTERING;
+            m.et = hit_eta;
             c.stack[n++] = hit;
         }
     }
-    c.sn = n;
+    m.sn = n;
+    return m;
 }
 
-// Lane state between scans.  The frames are in a device buffer, not compiler
-// scratch: scratch interleaves lanes per dword, so a store by the ~30 % of
-// lanes active in a shading branch dirties whole sectors of mostly-unchanged
-// neighbours and the write-back traffic is ~4x the bytes written; per-lane
-// contiguous frames only dirty the lane's own sectors.
+// Lane state between scans: the recursion level of its top node; its cold
+// frames (Params::frames, MAXF per lane, contiguous) are addressed from the
+// workgroup / lane ids where they are used rather than kept in 2 VGPRs across
+// the traversal.
 template <int MAXF>
 struct LaneState {
-    Frame<MAXF> *fr;                 // this lane's frames in Params::frames
+    void *frames;
     int top;                         // -1: primary ray pending
+    __device__ __forceinline__ Cold<MAXF> *cold() const {
+        // opaque: LLVM would otherwise hoist the address out of the
+        // persistent loop and keep it in a (spilled) VGPR pair
+        unsigned t;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
+        return reinterpret_cast<Cold<MAXF> *>(frames) + ((size_t)blockIdx.x * kBlock + t) * MAXF;
+    }
 };
 
+__device__ __forceinline__ void shadow_query(Query &q, const Params &p, int light, int self) {
+    V3 L, sd;
+    float dl;
+    bool unb;
+    light_vectors(p.lights[light], q.o, L, sd, dl, unb);
+    q.d = sd;
+    q.tmin = p.eps;
+    q.tmax = dl;
+    q.unb = unb;
+    q.self = self;
+    q.closest = false;
+    q.skipchk = false;
+    q.skipped = false;
+    q.win = -1;
+}
+
+__device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d) {
+    q.d = d;
+    q.tmin = p.eps;
+    q.tmax = kFltMax;
+    q.unb = false;
+    q.self = -1;
+    q.closest = true;
+    q.skipchk = false;
+    q.skipped = false;
+    q.win = -1;
+}
+
 // Advance one lane after its scan: consume the result, run ShadeRay logic
-// until the next TraceRay (returns true with q set up) or until the pixel is
-// done (returns false with `color` set).
-// Returns the kind of the TraceRay it set up in q (RK_SHADOW/RK_REFR/RK_REFL),
-// or RK_NONE when the pixel is finished (`color` set).
+// until the next TraceRay (returns its kind, RK_SHADOW/RK_REFR/RK_REFL, with q
+// set up) or until the pixel is done (returns RK_NONE with `color` set).
+// Invariant: while a node is on top, q.o is its hit point.
 template <int MAXF>
 __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
     int top = ls.top;
-    // a closest hit opens frame `top` (primary hit, refraction or reflection
+    HotR h;
+    // a closest hit opens node `top` (primary hit, refraction or reflection
     // child); its ShadeRay prologue runs at ONE call site below, so a wave
-    // whose lanes open frames for different reasons runs it once
-    bool begin = false;
+    // whose lanes open nodes for different reasons runs it once
+    bool open = false;
+    Medium m;
     // ---- consume the scan result ----
     if (top < 0) {                                   // primary (main.cpp:729-758)
         if (q.win < 0) {
             color = bkg;
             return RK_NONE;
         }
-        Frame<MAXF> &f = ls.fr[0];
-        f.obj = q.win;
-        f.ei = p.eta_bkg;
-        f.et = p.objs[q.win].eta;
-        f.sn = 1;
-        f.stack[0] = q.win;
-        f.state = ENTERING;
-        begin = true;
+        m = Medium{ENTERING, 1, p.eta_bkg, p.objs[q.win].eta};
+        ls.cold()[0].stack[0] = q.win;
+        open = true;
         top = 0;
     } else {
-        Frame<MAXF> &f = ls.fr[top];
-        // The fields the shadow-result path needs, loaded in ONE batch with
-        // the phase (pinned: the compiler would sink them under the branch and
-        // make them a second dependent round trip).  For a shadow result the
-        // query itself still holds the frame's hit point (q.o = P) and object
-        // (q.self), so those are not loaded at all.
-        const int phase = f.phase;
-        int light = f.light;
-        V3 fI = f.I, fN = f.N;
-        C3 fdif = f.dif, facc = f.acc;
-        asm volatile("" ::"v"(phase), "v"(light), "v"(fI.x), "v"(fI.y), "v"(fI.z), "v"(fN.x), "v"(fN.y),
-                     "v"(fN.z), "v"(fdif.r), "v"(fdif.g), "v"(fdif.b), "v"(facc.r), "v"(facc.g), "v"(facc.b));
+        lds_load(h);
+        const int phase = h_phase(h);
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
+            const int light = h_light(h);
             const LightK &lt = p.lights[light];
             // L as light_vectors computed it for the shadow ray just traced:
             // that ray's direction for a point light, the constant -L for a
             // directional one (q.d is not modified by a trace)
             V3 L = lt.w == 0.0f ? V3{lt.L[0], lt.L[1], lt.L[2]} : q.d;
-            const ObjK &ob = p.objs[q.self];
+            const ObjK &ob = p.objs[h.obj];
             // H only feeds the specular power: rsqrt instead of 3 IEEE
             // divisions (<= 2 ulp; vnorm(0) = NaN either way)
-            V3 h = vadd(L, fI);
-            V3 H = vmul(h, __builtin_amdgcn_rsqf(vdot(h, h)));
-            C3 dc = cmulf(cmulf(fdif, ob.kd), max0(vdot(fN, L)));
-            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(fN, H)), ob.n));
+            V3 hv = vadd(L, h.I);
+            V3 H = vmul(hv, __builtin_amdgcn_rsqf(vdot(hv, hv)));
+            C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
+            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
             C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
-            facc = cadd(facc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
-            light++;
-            f.acc = facc;
-            f.light = light;
-            if (light < p.nl) {
+            h.acc = cadd(h.acc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
+            h.meta += 1u << 9;                       // next light
+            if (light + 1 < p.nl) {
                 // next light's shadow ray from the same point: origin, self
                 // and cumulative mask are already in q (main.cpp:885-928)
-                V3 L2, sd;
-                float dl;
-                bool unb;
-                light_vectors(p.lights[light], q.o, L2, sd, dl, unb);
-                q.d = sd;
-                q.tmin = p.eps;
-                q.tmax = dl;
-                q.unb = unb;
-                q.closest = false;
-                q.skipchk = false;
-                q.skipped = false;
-                q.win = -1;
+                lds_store_light(h);
+                shadow_query(q, p, light + 1, h.obj);
                 ls.top = top;
                 return RK_SHADOW;
             }
-        } else if (f.phase == PH_REFR) {
-            const ObjK &ob = p.objs[f.obj];
+        } else if (phase == PH_REFR) {
             if (q.skipped) {
                 cnt.skip++;                          // tmp_transparency stays 0
-                f.phase = PH_REFL;
+                set_phase(h, PH_REFL);
             } else if (q.win >= 0) {
-                Frame<MAXF> &c = ls.fr[top + 1];
-                refr_transition(p, f, c, q.win, cnt);
-                c.obj = q.win;
-                f.phase = PH_REFR_CHILD;
-                begin = true;
-                top++;
+                m = refr_transition(p, h, ls.cold()[top], ls.cold()[top + 1], q.win, cnt);
+                set_phase(h, PH_REFR_CHILD);
+                open = true;
             } else {
-                C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)f.Ft)), (float)(1.0 - (double)ob.opacity));
-                f.acc = cadd(f.acc, tr);
-                f.phase = PH_REFL;
+                const ObjK &ob = p.objs[h.obj];
+                C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)h.dif.r)), (float)(1.0 - (double)ob.opacity));
+                h.acc = cadd(h.acc, tr);
+                set_phase(h, PH_REFL);
             }
-        } else if (f.phase == PH_REFL) {
+        } else {                                     // PH_REFL
             if (q.win >= 0) {
-                Frame<MAXF> &c = ls.fr[top + 1];
-                refl_transition(p, f, c, q.win);
-                c.obj = q.win;
-                f.phase = PH_REFL_CHILD;
-                begin = true;
-                top++;
+                m = refl_transition(p, h, ls.cold()[top], ls.cold()[top + 1], q.win);
+                set_phase(h, PH_REFL_CHILD);
+                open = true;
             } else {
                 // miss: refl = bkg * F_r; finish this node below
-                const ObjK &ob = p.objs[f.obj];
-                float F0 = (ob.eta - 1) / (ob.eta + 1);
-                float Fr = schlick(F0 * F0, f.cosI);
-                f.acc = cadd(f.acc, cmulf(bkg, Fr));
-                f.phase = PH_REFL_CHILD + 1;         // done
+                h.acc = cadd(h.acc, cmulf(bkg, refl_fresnel(p.objs[h.obj], cos_i(h))));
+                set_phase(h, PH_DONE);
             }
         }
+        if (open) {                                  // the recursion: save the parent
+            cold_save(ls.cold()[top], q.o, h);
+            top++;
+        }
     }
-    if (begin) node_begin(p, ls.fr[top], q.o, q.d, q.tmax);
-    // ---- run the current frame forward ----
+    if (open) {
+        q.o = node_open(p, q.win, q.o, q.d, q.tmax, m);
+        ls.top = top;
+        if (p.nl > 0) {                              // shadow ray for light 0 (main.cpp:885-928)
+            shadow_query(q, p, 0, q.win);
+            q.mask = C3{1.0f, 1.0f, 1.0f};           // the node's first light (main.cpp:788)
+            return RK_SHADOW;
+        }
+        lds_load(h);                                 // no lights: straight to the light loop's end
+    }
+    // ---- run the top node forward (phase PH_LIGHT here: its last light is done) ----
     for (;;) {
-        Frame<MAXF> &f = ls.fr[top];
-        const ObjK &ob = p.objs[f.obj];
-        if (f.phase == PH_LIGHT) {
-            if (f.light < p.nl) {                    // shadow ray for light f.light
-                V3 L, sd;
-                float dl;
-                bool unb;
-                light_vectors(p.lights[f.light], f.P, L, sd, dl, unb);
-                q.o = f.P;
-                q.d = sd;
-                q.tmin = p.eps;
-                q.tmax = dl;
-                q.unb = unb;
-                q.self = f.obj;
-                q.closest = false;
-                q.skipchk = false;
-                q.skipped = false;
-                q.win = -1;
-                q.mask = C3{1.0f, 1.0f, 1.0f};   // the node's first light (main.cpp:788)
-                ls.top = top;
-                return RK_SHADOW;
-            }
+        const ObjK &ob = p.objs[h.obj];
+        if (h_phase(h) == PH_LIGHT) {
             // ambient + specular sum, then Fresnel / transmission (main.cpp:961-992)
-            f.acc = cadd(cmulf(f.dif, ob.ka), f.acc);
-            float snell = f.ei / f.et;
-            float crit = asinf(f.et / f.ei);
-            float inc = acosf(f.cosI);
+            h.acc = cadd(cmulf(h.dif, ob.ka), h.acc);
+            const float cosI = cos_i(h);
+            float snell = h.ei / h.et;
+            float crit = asinf(h.et / h.ei);
+            float inc = acosf(cosI);
             bool tir = (crit < inc) && ((double)inc < kRightAngle);
-            float F0 = (f.et - f.ei) / (f.et + f.ei);
-            f.Ft = schlick(F0 * F0, f.cosI);
+            float F0 = (h.et - h.ei) / (h.et + h.ei);
+            h.dif.r = schlick(F0 * F0, cosI);        // F_t (the diffuse colour is no longer needed)
             if (p.depth - top > 0 && !tir && (double)ob.opacity < 1.0 && ob.eta > 0) {
-                float k = sqrtf((float)(1.0 - (double)(snell * snell) * (1.0 - (double)(f.cosI * f.cosI))));
-                V3 T = vadd(vmul(vmul(f.N, -1.0f), k), vmul(vsub(vmul(f.N, f.cosI), f.I), snell));
-                q.o = f.P;
-                q.d = T;
-                q.tmin = p.eps;
-                q.tmax = kFltMax;
-                q.unb = false;
-                q.self = -1;
-                q.closest = true;
-                q.skipchk = (f.sn > 0) && !ob.is_sphere;
-                q.back = f.sn > 0 ? f.stack[f.sn - 1] : -1;
-                q.skipped = false;
-                q.win = -1;
-                f.phase = PH_REFR;
+                float k = sqrtf((float)(1.0 - (double)(snell * snell) * (1.0 - (double)(cosI * cosI))));
+                V3 T = vadd(vmul(vmul(h.N, -1.0f), k), vmul(vsub(vmul(h.N, cosI), h.I), snell));
+                closest_query(q, p, T);
+                const int sn = h_sn(h);
+                q.skipchk = (sn > 0) && !ob.is_sphere;
+                q.back = sn > 0 ? ls.cold()[top].stack[sn - 1] : -1;
+                set_phase(h, PH_REFR);
+                lds_store_phase(h);
                 ls.top = top;
                 return RK_REFR;
             }
-            f.phase = PH_REFL;
+            set_phase(h, PH_REFL);
         }
-        if (f.phase == PH_REFL) {                    // main.cpp:1103-1124
-            float F0 = (ob.eta - 1) / (ob.eta + 1);
-            float Fr = schlick(F0 * F0, f.cosI);
+        if (h_phase(h) == PH_REFL) {                 // main.cpp:1103-1124
+            const float cosI = cos_i(h);
+            float Fr = refl_fresnel(ob, cosI);
             if (p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
-                V3 R = vsub(vmul(f.N, (float)(2.0 * (double)f.cosI)), f.I);
-                q.o = f.P;
-                q.d = R;
-                q.tmin = p.eps;
-                q.tmax = kFltMax;
-                q.unb = false;
-                q.self = -1;
-                q.closest = true;
-                q.skipchk = false;
-                q.skipped = false;
-                q.win = -1;
+                V3 R = vsub(vmul(h.N, (float)(2.0 * (double)cosI)), h.I);
+                closest_query(q, p, R);
+                lds_store_phase(h);
                 ls.top = top;
                 return RK_REFL;
             }
-            f.phase = PH_REFL_CHILD + 1;
+            set_phase(h, PH_DONE);
         }
         // node complete: ((dka + spec) + trans) + refl already folded into acc
-        C3 c = f.acc;
+        const C3 c = h.acc;
         if (top == 0) {
             color = c;
             ls.top = -1;
             return RK_NONE;
         }
         top--;
-        Frame<MAXF> &pf = ls.fr[top];
-        const ObjK &pob = p.objs[pf.obj];
-        if (pf.phase == PH_REFR_CHILD) {             // main.cpp:1072-1083
-            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)pf.Ft)), (float)(1.0 - (double)pob.opacity));
-            pf.acc = cadd(pf.acc, tr);
-            pf.phase = PH_REFL;
+        q.o = cold_restore(ls.cold()[top], h);
+        const ObjK &pob = p.objs[h.obj];
+        if (h_phase(h) == PH_REFR_CHILD) {           // main.cpp:1072-1083
+            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)h.dif.r)), (float)(1.0 - (double)pob.opacity));
+            h.acc = cadd(h.acc, tr);
+            set_phase(h, PH_REFL);
         } else {                                     // PH_REFL_CHILD, main.cpp:1184-1194
-            float F0 = (pob.eta - 1) / (pob.eta + 1);
-            float Fr = schlick(F0 * F0, pf.cosI);
-            pf.acc = cadd(pf.acc, cmulf(c, Fr));
-            pf.phase = PH_REFL_CHILD + 1;
+            h.acc = cadd(h.acc, cmulf(c, refl_fresnel(pob, cos_i(h))));
+            set_phase(h, PH_DONE);
         }
+        lds_store(h);                                // the parent is the top node again
     }
 }
 
@@ -1001,7 +1135,9 @@ __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, 
 template <int MAXF, int MODE>
 __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) {
     constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
-    extern __shared__ float4 lds[];
+    // LDS: every lane's shading state (kLdsHot words, kBlock apart), then the
+    // staged primitives (MODE_SCAN_LDS) or the BVH traversal stacks (MODE_BVH)
+    float4 *lds = rt_lds + kLdsHot * kBlock / 4;
     const float4 *lds_f = lds;
     const float4 *lds_s = lds + 5 * p.nf;
     if (SRC_LDS) {
@@ -1013,9 +1149,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
-    ls.fr = reinterpret_cast<Frame<MAXF> *>(p.frames) + ((size_t)blockIdx.x * kBlock + threadIdx.x) * MAXF;
+    ls.frames = p.frames;
     Counters cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
+    unsigned w_known = 0, w_bf = 0;
     int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
     if (MODE == MODE_BVH) stk[0] = rtbvh::kEmpty;           // bvh_trace's stack bottom (never overwritten)
     Query q;
@@ -1108,6 +1245,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
         w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
+        w_known += (unsigned)__popcll(__ballot(known));
         if (MODE == MODE_BVH) {
             q.bf = search && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
 #if RT_PROF
@@ -1126,7 +1264,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_trace += c2 - c1;
 #endif
             bool need = search && q.bf;
-            if (__ballot(need)) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
+            const unsigned long long nb = __ballot(need);
+            w_bf += (unsigned)__popcll(nb);
+            if (nb) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
 #if RT_PROF
             pc_bf += __builtin_amdgcn_s_memtime() - c2;
 #endif
@@ -1140,6 +1280,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[1], w_shadow);
         atomicAdd(&st[2], w_refr);
         atomicAdd(&st[3], w_refl);
+        atomicAdd(&st[32], (unsigned long long)w_known);
+        atomicAdd(&st[33], (unsigned long long)w_bf);
     }
     atomicAdd(&st[4], (unsigned long long)cnt.skip);
     atomicAdd(&st[5], (unsigned long long)cnt.ub);
@@ -1262,10 +1404,10 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
 V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
-    if (mode == MODE_SCAN_LDS) return s->lds_bytes;
-    if (mode == MODE_BVH)
-        return (size_t)(s->bvh_stack + 2) * kBlock * sizeof(int);   // + sentinel + spare
-    return 0;
+    size_t shade = (size_t)kLdsHot * kBlock * sizeof(float);         // per-lane shading state
+    if (mode == MODE_SCAN_LDS) return shade + s->lds_bytes;
+    if (mode == MODE_BVH) return shade + (size_t)s->base.stack_cap * kBlock * sizeof(int);
+    return shade;
 }
 
 template <int MAXF, int MODE>
@@ -1279,7 +1421,8 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
     Params pl = p;
-    size_t fbytes = (size_t)grid * kBlock * MAXF * sizeof(Frame<MAXF>);
+    const size_t cold_bytes = (size_t)grid * kBlock * MAXF * sizeof(Cold<MAXF>);
+    size_t fbytes = cold_bytes + (size_t)grid * kBlock * kStack * sizeof(int);
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
@@ -1293,6 +1436,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
         }
     }
     pl.frames = slot.d_frames;
+    pl.ovf = reinterpret_cast<int *>(static_cast<char *>(slot.d_frames) + cold_bytes);
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
     s->last_lds = (long long)shm;
@@ -1695,6 +1839,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     for (int i = 0; i < desc->n_lights; i++)
         if (desc->lights[i].w == 0.0f && ns > 0) p.dir_bf = 1;
     p.shadow_early_out = nan_fac ? 0 : 1;
+    p.stack_cap = kLdsStackDefault;
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
     *out = s;
     return RT_OK;
@@ -1725,6 +1870,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
     else if (k == "inflight") return set_inflight(s, value);
+    else if (k == "lds_stack") {
+        if (value < 12 || value > kLdsStack) return RT_E_INVALID;
+        s->base.stack_cap = (int)value;
+    }
     else if (k == "bvh_leaf" || k == "bvh_trav") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else s->opt_bvh_trav = std::max(0LL, value);
@@ -1828,6 +1977,10 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     stats->box_tests = h[6];
     stats->face_tests = h[7];
     stats->sphere_tests = h[8];
+    stats->shadow_known = h[32];
+    stats->bf_queries = h[33];
+    stats->stack_spills = h[34];
+    stats->bvh_build_ms = s->bvh_build_ms;
     // device time of the launch: first wave start .. last wave end (100 MHz
     // clock); the events' interval also holds any wait for a previous frame
     // still on the CUs

@@ -70,7 +70,9 @@ class rt_stats(C.Structure):
                 ("refraction", C.c_ulonglong), ("reflection", C.c_ulonglong),
                 ("skip_trans", C.c_ulonglong), ("ub_back", C.c_ulonglong),
                 ("kernel_ms", C.c_double), ("box_tests", C.c_ulonglong),
-                ("face_tests", C.c_ulonglong), ("sphere_tests", C.c_ulonglong)]
+                ("face_tests", C.c_ulonglong), ("sphere_tests", C.c_ulonglong),
+                ("shadow_known", C.c_ulonglong), ("bf_queries", C.c_ulonglong),
+                ("stack_spills", C.c_ulonglong), ("bvh_build_ms", C.c_double)]
 
     def rays(self) -> int:
         return int(self.primary + self.shadow + self.refraction + self.reflection)
@@ -322,8 +324,11 @@ class GpuScene:
 
     def debug_counters(self) -> list[int]:
         """Raw device counters of the last render (rt_scene_debug_counters)."""
-        buf = (C.c_ulonglong * 32)()
-        _check(hip_lib().rt_scene_debug_counters(self._h, buf, 32), "rt_scene_debug_counters")
+        buf = (C.c_ulonglong * 40)()
+        rc = hip_lib().rt_scene_debug_counters(self._h, buf, 40)
+        if rc == -1:                  # a library of round 1 (A/B baselines) has 32 slots
+            rc = hip_lib().rt_scene_debug_counters(self._h, buf, 32)
+        _check(rc, "rt_scene_debug_counters")
         return list(buf)
 
 

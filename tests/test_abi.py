@@ -37,7 +37,7 @@ def test_struct_sizes_match_c():
     assert C.sizeof(rtamd.rt_sphere_desc) == 4 * 4 + 48 + 4
     assert C.sizeof(rtamd.rt_face_desc) == (9 + 9 + 6) * 4 + 4 + 48 + 4
     assert C.sizeof(rtamd.rt_camera) == 48
-    assert C.sizeof(rtamd.rt_stats) == 6 * 8 + 8 + 3 * 8
+    assert C.sizeof(rtamd.rt_stats) == 6 * 8 + 8 + 3 * 8 + 3 * 8 + 8
 
 
 def test_strerror_without_device():
