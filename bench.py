@@ -43,6 +43,9 @@ WORKLOADS = {
     "C3": "C3: 4096x4096, 1000 spheres + 1000 triangles, reflection+refraction depth 4, 2 point lights",
     "C4": "C4: 8192x8192, 10k textured triangles, 1 directional + 1 point light (hard shadows)",
     "C5": "C5: 16384x16384, 100k spheres, reflection+refraction depth 8",
+    "C3D": "C3 with a directional light (1,-1,-1) + a point light: unnormalised directional shadow rays "
+           "against spheres (main.cpp:895)",
+    "C3G": "C3 with 10% glass triangles: face-incident refraction, SKIP_TRANS (main.cpp:1000-1002)",
 }
 
 

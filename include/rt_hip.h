@@ -173,6 +173,15 @@ int rt_scene_prepare(rt_scene *scene, const rt_camera *cam, int W, int H);
 int rt_render_row_blocks(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,
                          int nrows, float *out_rgb, rt_stats *stats);
 
+/* Put gathered row sets back in image order, on the device (the multi-device
+ * CLI: after an RCCL gather of every device's rt_render_row_blocks buffer).
+ * gathered holds `world` buffers of rows_per * W * 3 floats, buffer r being
+ * rank r's rows as rth_row_set deals them (blocks of `block` rows, round
+ * robin); image receives H * W * 3 floats.  Both are device memory of the
+ * current device; asynchronous on hip_stream. */
+int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
+                         void *hip_stream);
+
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
  * (persistent blocks, 0 = occupancy), "reserve" (block slots the occupancy-

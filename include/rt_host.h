@@ -55,6 +55,15 @@ int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads)
 /* remove_extension(path) + ".ppm" (src/utility.h:34-41, main.cpp:614-616). */
 int rth_output_path(const char *scene_path, char *out, int outlen);
 
+/* Multi-device row sharding of a H-row image (the reference's row loop
+ * main.cpp:718, split): rows are dealt in blocks of `block` rows round robin,
+ * so device `rank` of `world` renders local rows k = 0..nrows-1 = image rows
+ * y0 + (k / block) * step + k % block, with y0 = rank * block and
+ * step = block * world (the arguments of rt_render_row_blocks).  rows_per is
+ * the largest rank's row count (equal-size buffers for one gather).  Returns
+ * 0, or -1 for bad arguments. */
+int rth_row_set(int H, int world, int rank, int block, int *y0, int *step, int *nrows, int *rows_per);
+
 #ifdef __cplusplus
 }
 #endif

@@ -280,8 +280,9 @@ inline void leaf_decode(int32_t link, int &off, int &nfaces, int &count) {
     count = v & 15;
 }
 template <int W, class IsFace, class Emit>
-inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace is_face, Emit emit) {
-    size_t words = 0;
+inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace is_face, Emit emit,
+                         size_t base_words = 0) {
+    size_t words = base_words;            // the stream may already hold other trees' records
     for (NodeW<W> &n : Q.nodes) {
         for (int i = 0; i < W; i++) {
             int32_t l = n.link[i];

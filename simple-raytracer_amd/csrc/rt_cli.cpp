@@ -7,8 +7,11 @@
 //   missing command      -> stdout "Error: Requires ...", 0  (main.cpp:574-602)
 //   bad command          -> std::cerr lines, uncaught exception (abort)
 // New optional flags (the reference has none): --depth N, --imsize W H,
-// --gpus N (row strips rendered on N devices concurrently), --device D,
-// --float-out FILE (raw float32 H*W*3 framebuffer), --stats.
+// --gpus N (rows dealt to N devices in 8-row blocks), --device D,
+// --gather rccl|host (how the devices' rows come together; default rccl for
+// N > 1: one RCCL gather to the first device over xGMI, a device-side
+// de-interleave and one copy to the host; host: each device copies its rows
+// to the host), --float-out FILE (raw float32 H*W*3 framebuffer), --stats.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,8 +22,101 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
 #include "rt_hip.h"
 #include "rt_host.h"
+
+namespace {
+
+const int kRowBlock = 8;
+
+// One process, N devices: every device renders its row set (rth_row_set)
+// into HBM, one RCCL gather collects the N buffers on the first device, a
+// device-side de-interleave puts the rows in image order, one copy brings the
+// image to the host.  The seam is the reference's single render call
+// (main.cpp:607), its row loop (main.cpp:718) split across the devices.
+int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, int gpus, std::vector<float> &img,
+                std::vector<rt_stats> &st) {
+    struct Dev {
+        int id = 0;
+        rt_scene *scene = nullptr;
+        hipStream_t stream = nullptr;
+        float *strip = nullptr, *recv = nullptr, *image = nullptr;
+        int y0 = 0, step = 0, nrows = 0, rows_per = 0;
+    };
+    std::vector<Dev> d(gpus);
+    std::vector<int> ids(gpus);
+    std::vector<ncclComm_t> comms(gpus, nullptr);
+    int rc = 0;
+    auto fail = [&](const char *what, int code) {
+        if (!rc) {
+            std::cerr << "rt: " << what << " failed (" << code << ")" << std::endl;
+            rc = 3;
+        }
+    };
+    for (int g = 0; g < gpus && !rc; g++) {
+        Dev &v = d[g];
+        v.id = ids[g] = device + g;
+        if (rth_row_set(H, gpus, g, kRowBlock, &v.y0, &v.step, &v.nrows, &v.rows_per)) fail("row set", -1);
+        if (hipSetDevice(v.id) != hipSuccess) fail("hipSetDevice", v.id);
+        int e = rt_scene_create(v.id, rth_desc(hs), &v.scene);
+        if (e) fail(rt_strerror(e), e);
+        const size_t strip = (size_t)v.rows_per * W * 3 * sizeof(float);
+        if (!rc && (hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking) != hipSuccess ||
+                    hipMalloc(&v.strip, strip) != hipSuccess))
+            fail("device buffers", g);
+        if (!rc && g == 0 && (hipMalloc(&v.recv, strip * gpus) != hipSuccess ||
+                              hipMalloc(&v.image, (size_t)W * H * 3 * sizeof(float)) != hipSuccess))
+            fail("gather buffers", g);
+    }
+    if (!rc) {
+        ncclResult_t r = ncclCommInitAll(comms.data(), gpus, ids.data());
+        if (r != ncclSuccess) fail(ncclGetErrorString(r), (int)r);
+    }
+    for (int g = 0; g < gpus && !rc; g++) {
+        Dev &v = d[g];
+        (void)hipSetDevice(v.id);
+        if (v.nrows > 0) {
+            int e = rt_render_row_blocks_async(v.scene, &cam, W, H, v.y0, kRowBlock, v.step, v.nrows, v.strip,
+                                               v.stream);
+            if (e) fail(rt_strerror(e), e);
+        }
+    }
+    if (!rc) {
+        const size_t count = (size_t)d[0].rows_per * W * 3;
+        ncclGroupStart();
+        for (int g = 0; g < gpus; g++)
+            ncclGather(d[g].strip, g == 0 ? d[0].recv : nullptr, count, ncclFloat32, 0, comms[g], d[g].stream);
+        ncclResult_t r = ncclGroupEnd();
+        if (r != ncclSuccess) fail(ncclGetErrorString(r), (int)r);
+    }
+    if (!rc) {
+        (void)hipSetDevice(d[0].id);
+        int e = rt_deinterleave_rows(d[0].recv, gpus, d[0].rows_per, W, H, kRowBlock, d[0].image, d[0].stream);
+        if (e) fail(rt_strerror(e), e);
+        if (!rc && (hipMemcpyAsync(img.data(), d[0].image, img.size() * sizeof(float), hipMemcpyDeviceToHost,
+                                   d[0].stream) != hipSuccess ||
+                    hipStreamSynchronize(d[0].stream) != hipSuccess))
+            fail("image copy", 0);
+    }
+    for (int g = 0; g < gpus; g++) {
+        Dev &v = d[g];
+        (void)hipSetDevice(v.id);
+        if (v.stream) (void)hipStreamSynchronize(v.stream);
+        if (!rc && v.scene && v.nrows > 0 && rt_scene_last_stats(v.scene, &st[g])) fail("stats", g);
+        if (comms[g]) ncclCommDestroy(comms[g]);
+        if (v.strip) (void)hipFree(v.strip);
+        if (v.recv) (void)hipFree(v.recv);
+        if (v.image) (void)hipFree(v.image);
+        if (v.stream) (void)hipStreamDestroy(v.stream);
+        if (v.scene) rt_scene_destroy(v.scene);
+    }
+    return rc;
+}
+
+}  // namespace
 
 int main(int argc, char *argv[]) {
     if (argc <= 1) {
@@ -30,6 +126,7 @@ int main(int argc, char *argv[]) {
     }
     int depth = -1, W = -1, H = -1, gpus = 1, device = 0;
     bool stats = false;
+    std::string gather;
     const char *float_out = nullptr;
     for (int i = 2; i < argc; i++) {
         std::string a = argv[i];
@@ -38,6 +135,7 @@ int main(int argc, char *argv[]) {
         else if (a == "--gpus" && i + 1 < argc) gpus = atoi(argv[++i]);
         else if (a == "--device" && i + 1 < argc) device = atoi(argv[++i]);
         else if (a == "--float-out" && i + 1 < argc) float_out = argv[++i];
+        else if (a == "--gather" && i + 1 < argc) gather = argv[++i];
         else if (a == "--stats") stats = true;
     }
     rth_scene *hs = nullptr;
@@ -74,17 +172,25 @@ int main(int argc, char *argv[]) {
     }
     if (gpus < 1) gpus = 1;
     if (gpus > ndev - device) gpus = ndev - device;
+    if (gather.empty()) gather = gpus > 1 ? "rccl" : "host";
+    if (gather != "rccl" && gather != "host") {
+        std::cerr << "rt: --gather must be rccl or host" << std::endl;
+        return 2;
+    }
     std::vector<float> img((size_t)W * H * 3);
     std::vector<rt_stats> st(gpus);
     std::vector<int> rcs(gpus, 0);
     std::vector<std::thread> pool;
-    // One host thread per device.  One device renders the image in one call;
-    // several deal the rows out in 8-row blocks, round robin (device g gets
-    // blocks g, g+N, ...: every device the same mix of cheap and costly rows),
-    // each renders its row set into a buffer of its own and the blocks are
-    // put back in image order.
-    const int kRowBlock = 8;
-    for (int g = 0; g < gpus; g++) {
+    if (gather == "rccl") {
+        int r = render_rccl(hs, cam, W, H, device, gpus, img, st);
+        if (r) return r;
+    }
+    // --gather host: one host thread per device.  One device renders the image
+    // in one call; several deal the rows out in 8-row blocks, round robin
+    // (device g gets blocks g, g+N, ...: every device the same mix of cheap
+    // and costly rows), each renders its row set into a buffer of its own and
+    // the blocks are put back in image order on the host.
+    for (int g = 0; g < gpus && gather == "host"; g++) {
         pool.emplace_back([&, g] {
             rt_scene *s = nullptr;
             int r = rt_scene_create(device + g, rth_desc(hs), &s);

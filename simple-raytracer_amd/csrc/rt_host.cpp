@@ -562,3 +562,21 @@ int rth_output_path(const char *scene_path, char *out, int outlen) {
 }
 
 }  // extern "C"
+
+extern "C" int rth_row_set(int H, int world, int rank, int block, int *y0, int *step, int *nrows, int *rows_per) {
+    if (H < 1 || world < 1 || rank < 0 || rank >= world || block < 1 || !y0 || !step || !nrows || !rows_per)
+        return -1;
+    const int nblocks = (H + block - 1) / block;
+    auto rows_of = [&](int r) {
+        int n = 0;
+        for (int b = r; b < nblocks; b += world) n += std::min(block, H - b * block);
+        return n;
+    };
+    *y0 = rank * block;
+    *step = block * world;
+    *nrows = rows_of(rank);
+    int mx = 1;
+    for (int r = 0; r < world; r++) mx = std::max(mx, rows_of(r));
+    *rows_per = mx;
+    return 0;
+}

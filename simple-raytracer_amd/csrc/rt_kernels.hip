@@ -121,7 +121,18 @@ struct LightK {
 };
 struct TexK {
     int w, h;
-    long long off;
+    int tiles_x;                         // 8x8-texel tiles per tile row
+    int pad;
+    long long off;                       // first texel word in Params::texels
+};
+// directional light: its shadow-region tree over the spheres (rt host:
+// dir_trees) -- root node in Params::bvh (-1: no sphere can shadow) and the
+// rotation R (rows) into the frame the tree's boxes were built in
+struct DirK {
+    float R[9];
+    int root;
+    float cone_k;                        // max(0, |d|^2 - 1), rounded up
+    float cone_h;                        // |d| < 1: height bound of the shadow region, else +inf
 };
 
 struct Params {
@@ -131,7 +142,7 @@ struct Params {
     const ObjK *__restrict__ objs;
     const FaceShadeK *__restrict__ fsh;
     const LightK *__restrict__ lights;
-    const unsigned char *__restrict__ texels;
+    const unsigned *__restrict__ texels; // all textures: RGBA8 words in 8x8-texel tiles
     const TexK *__restrict__ texs;
     float *__restrict__ out;
     unsigned int *__restrict__ work;     // pixel work counter
@@ -147,7 +158,9 @@ struct Params {
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
-    int dir_bf;                          // directional shadow rays must scan spheres brute force
+    int dir_bf;                          // directional lights in a scene with spheres: 0 none,
+                                         // 1 brute-force scan, 2 faces by the BVH + shadow-region trees
+    const DirK *__restrict__ dirk;       // per light (dir_bf == 2)
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int bvh_stack;                       // BVH: worst-case traversal stack entries of the tree
     int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
@@ -310,6 +323,30 @@ struct Counters {
 };
 enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY = 4 };
 
+// Nearest root of object `obj` alone along q with tmin < t < FLT_MAX
+// (kFltMax: none) -- the minimum the reference's in-order scan holds once it
+// has passed that object (main.cpp:997, :1004).
+__device__ __forceinline__ float own_nearest(const Query &q, const Params &p, int obj, Counters &cnt) {
+    float tb = kFltMax;
+    if (obj < p.nf) {
+        const float4 *F = p.fscan + 5 * obj;
+        float t, a, b, g;
+        cnt.ftests++;
+        if (face_test(F[0], F[1], F[2], F[3], F[4], q.o, q.d, t, a, b, g) & (F[1].w != 0.0f) & (t > q.tmin) &
+            (t < kFltMax))
+            tb = t;
+    } else {
+        float t1, t2;
+        cnt.stests++;
+        if (sphere_test(p.sscan[obj - p.nf], q.o, q.d, t1, t2)) {
+            if ((t1 > q.tmin) & (t1 < tb)) tb = t1;
+            if ((t2 > q.tmin) & (t2 < tb)) tb = t2;
+        }
+    }
+    return tb;
+}
+
+
 constexpr int kNodeF4 = 4;                       // float4 per quantised 4-wide node (rt_bvh.h Node4Q)
 constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
 constexpr int kNStats = 40;                      // device counter slots (rt_scene_debug_counters)
@@ -322,10 +359,11 @@ __device__ __forceinline__ float safe_rcp(float x) {
 // rt_bvh.h leaf_records.  Closest: running (best, win); shadow: every valid
 // hit multiplies the mask (an opaque one ends the ray).
 __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, Counters &cnt, float &best, int &win,
-                                           bool &opaque) {
+                                           bool &opaque, bool faces_only) {
     int v = -link - 1;
     const float4 *R = p.leafrec + (v >> 8);
     int nfc = (v >> 4) & 15, count = v & 15;
+    if (faces_only) count = nfc;             // the leaf's faces come first
     for (int k = 0; k < count; k++) {
         float t[2];
         int nt = 0;
@@ -362,6 +400,13 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
                     best = tt;
                     win = key;
                 }
+            } else if (q.skipchk) {
+                // SKIP_TRANS (main.cpp:997-1002): a candidate of another
+                // object that the reference's in-order scan would see as a
+                // new minimum -- any one before the stack top's object in
+                // order, or nearer than the stack top's own nearest root
+                // (q.tmax) -- aborts the refraction
+                if ((key != q.back) & (tt > q.tmin) & (tt < kFltMax) & ((key < q.back) | (tt < q.tmax))) opaque = true;
             } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
                 if (fac == 0.0f && p.shadow_early_out) {
                     opaque = true;
@@ -381,17 +426,30 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 // visited together.  Node visits stay one dependent fetch each, and the leaf
 // code runs with most lanes active instead of in almost every wave trip (+6 %
 // over an if-if loop).  The result does not depend on the visiting order.
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
+//
+// point: a CONE query instead of a ray (directional shadow rays against
+// spheres; dir_tree on the host) -- which boxes of the tree at `root` may
+// hold a sphere whose shadow region contains the point po (the origin in
+// the light's frame): the same traversal with direction (1, 1, 1), so that
+// the plane distances are the child boxes' offsets from po, and a cone test
+// per child instead of the slab test; its leaves are still tested with the
+// query's own ray (q.o, q.d).
+template <bool point>
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, int root = 0,
+                          V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
     // |1/d| capped at 2^100 (1/0 -> 1e30 as before): the quantised planes'
     // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
     // and the cap is conservative: an axis with |d| < 2^-100 moves the ray by
     // less than 2^-100 D along it, far inside the 2^-16 D primitive padding
-    const float ix = clampr(safe_rcp(q.d.x), -0x1p100f, 0x1p100f);
-    const float iy = clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
-    const float iz = clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
+    const float ix = point ? 1.0f : clampr(safe_rcp(q.d.x), -0x1p100f, 0x1p100f);
+    const float iy = point ? 1.0f : clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
+    const float iz = point ? 1.0f : clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
     const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
-    const float ox = q.o.x * ix, oy = q.o.y * iy, oz = q.o.z * iz;
-    const float tlo = q.tmin - fabsf(q.tmin) * 0x1p-16f;
+    const float ox = point ? po.x : q.o.x * ix, oy = point ? po.y : q.o.y * iy, oz = point ? po.z : q.o.z * iz;
+    const float tlo = point ? 0.0f : q.tmin - fabsf(q.tmin) * 0x1p-16f;
+    // directional shadow ray in a scene with spheres: this pass tests the
+    // faces only, the spheres come in the point pass
+    const bool faces_only = !point && !q.closest && !q.skipchk && q.unb && p.dir_bf == 2;
     float best = q.tmax;                       // closest: running min (kFltMax at start)
     int win = -1;
     bool opaque = false;
@@ -401,7 +459,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
     int node = rtbvh::kEmpty;                  // >= 0 inner node, < 0 leaf, kEmpty: done
     int leaf = rtbvh::kEmpty;                  // postponed leaf
     auto thi_now = [&] {
-        return q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
+        return point ? 0.0f : q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
     };
     // LDS holds stack entries [0, kLdsStack); entry 0 is kEmpty, or kRefill + b
     // when b blocks of kSpill older entries wait in device memory (ovf).
@@ -464,12 +522,25 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
             float tnx = fmaf((float)((nx >> sh) & 0xffu), Ax, Bx), tfx = fmaf((float)((fx >> sh) & 0xffu), Ax, Bx);
             float tny = fmaf((float)((ny >> sh) & 0xffu), Ay, By), tfy = fmaf((float)((fy >> sh) & 0xffu), Ay, By);
             float tnz = fmaf((float)((nz >> sh) & 0xffu), Az, Bz), tfz = fmaf((float)((fz >> sh) & 0xffu), Az, Bz);
-            float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
-            float tf = fminf(fminf(tfx, tfy), fminf(tfz, thi));
-            // entry distance of a hit child, +inf for a miss or an empty slot
-            // (unused slots link to the empty leaf, kEmptyLeaf: entering one is
-            // harmless, so no link test; their inverted boxes miss anyway)
-            k[i] = (tn <= tf) ? tn : kInf;
+            if (!point) {
+                float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
+                float tf = fminf(fminf(tfx, tfy), fminf(tfz, thi));
+                // entry distance of a hit child, +inf for a miss or an empty
+                // slot (unused slots link to the empty leaf, kEmptyLeaf:
+                // entering one is harmless, so no link test; their inverted
+                // boxes miss anyway)
+                k[i] = (tn <= tf) ? tn : kInf;
+            } else {
+                // shadow cone (see dir_tree): the child's box lies at offsets
+                // [tn, tf] from the origin po, z along the light; it may hold
+                // a shadowing sphere iff its top is not below po and its
+                // lateral distance d satisfies d^2 <= cone_k * top^2 (and,
+                // for a bounded region, its bottom is within cone_h)
+                float dx = fmaxf(fmaxf(tnx, -tfx), 0.0f), dy = fmaxf(fmaxf(tny, -tfy), 0.0f);
+                float d2 = fmaf(dx, dx, dy * dy);
+                bool in = (tfz >= 0.0f) & (d2 <= cone_k * (tfz * tfz)) & (tnz <= cone_h);
+                k[i] = in ? d2 : kInf;           // nearest the cone's axis first
+            }
         }
         // up to 3 pushes below write stk[sp .. sp + 2]: make room (rare)
         if (sp > p.stack_cap - 3) spill();
@@ -514,7 +585,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
     // (loads and stores share vmcnt, in order).
-    visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3));
+    if (point)
+        node = root;
+    else
+        visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3));
     for (;;) {
         while (node >= 0) {
 #if RT_PROF >= 2
@@ -537,7 +611,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
 #if RT_PROF
             cnt.trips++;
 #endif
-            leaf_visit(q, p, leaf, cnt, best, win, opaque);
+            leaf_visit(q, p, leaf, cnt, best, win, opaque, faces_only);
             leaf = rtbvh::kEmpty;
             if (opaque) {
                 node = rtbvh::kEmpty;
@@ -556,6 +630,8 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt) {
             q.tmax = best;
             q.win = win;
         }
+    } else if (q.skipchk) {
+        q.skipped = opaque;
     } else if (opaque) {
         q.mask = {0.0f, 0.0f, 0.0f};
     }
@@ -614,6 +690,7 @@ enum {
 extern __shared__ float4 rt_lds[];   // dynamic LDS of render_kernel: state, then stack / primitives
 
 __device__ __forceinline__ float *lane_lds() { return reinterpret_cast<float *>(rt_lds) + threadIdx.x; }
+__device__ __forceinline__ int h_light_lds() { return (int)(__float_as_uint(lane_lds()[LW_META * kBlock]) >> 9); }
 __device__ __forceinline__ void lds_load(HotR &h) {
     const float *l = lane_lds();
     h.N = {l[(LW_N + 0) * kBlock], l[(LW_N + 1) * kBlock], l[(LW_N + 2) * kBlock]};
@@ -712,9 +789,22 @@ __device__ void hit_geometry(const Params &p, int obj, V3 o, V3 d, float t, V3 &
     }
 }
 
-__device__ __forceinline__ float texel(const Params &p, const TexK &t, int x, int y, int c) {
-    float v = (float)p.texels[t.off + ((long long)y * t.w + x) * 3 + c];
-    return (v - 0.0f) * (1.0f - 0.0f) / (255.0f - 0.0f) + 0.0f;   // map(v, 0, 255, 0, 1)
+// Texel (x, y) of a texture -- the reference's nearest texel (main.cpp:816-818,
+// :850-852).  Textures live in HBM as one 32-bit word per texel (R, G, B
+// bytes) in 8x8-texel tiles (256 B, two cache lines): one load per texel
+// instead of three byte loads, and neighbouring texels -- what neighbouring
+// pixels fetch -- share lines in both directions.  (gfx950 exposes no image
+// arrays through HIP -- hipMallocArray: "operation not supported",
+// tools/tex_probe.hip -- so the texture unit's tiled image path is not
+// available; this is its layout in a plain buffer.)  Each channel then goes
+// through the reference's map(v, 0, 255, 0, 1) in float.
+__device__ __forceinline__ float tex_map(unsigned v) {
+    return ((float)v - 0.0f) * (1.0f - 0.0f) / (255.0f - 0.0f) + 0.0f;
+}
+__device__ __forceinline__ C3 texel_rgb(const Params &p, const TexK &t, int x, int y) {
+    const long long tile = (long long)(y >> 3) * t.tiles_x + (x >> 3);
+    const unsigned w = p.texels[t.off + tile * 64 + ((y & 7) << 3) + (x & 7)];
+    return C3{tex_map(w & 0xffu), tex_map((w >> 8) & 0xffu), tex_map((w >> 16) & 0xffu)};
 }
 
 // ShadeRay prologue (main.cpp:785-872): hit record, diffuse / texture and the
@@ -801,7 +891,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
                                 (float)((double)height - 1.0));
             int j = (int)clampr((float)round(((double)width - 1.0) * (double)u), 0.0f,
                                 (float)((double)width - 1.0));
-            dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
+            dif = texel_rgb(p, tx, j, i);
         } else {                                                     // main.cpp:834-861
             const FaceShadeK &fs = p.fsh[obj];
             float u = (bary.x * fs.vt[0][0]) + (bary.y * fs.vt[1][0]) + (bary.z * fs.vt[2][0]);
@@ -810,7 +900,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
             u = clampr(u, 0.0f, 1.0f);
             int i = (int)clampr(roundf((width - 1.0f) * u), 0.0f, (float)((double)width - 1.0));
             int j = (int)clampr(roundf((height - 1.0f) * v), 0.0f, (float)((double)height - 1.0));
-            dif = {texel(p, tx, i, j, 0), texel(p, tx, i, j, 1), texel(p, tx, i, j, 2)};
+            dif = texel_rgb(p, tx, i, j);
         }
     }
     if ((double)cosI < 0.0 && ob.is_sphere) {                      // main.cpp:869-872
@@ -992,11 +1082,13 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         const int phase = h_phase(h);
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
             const int light = h_light(h);
-            const LightK &lt = p.lights[light];
+            // the light's words in one batch (LightK: xyz w | col | L)
+            const f4v *lw = reinterpret_cast<const f4v *>(p.lights + light);
+            const f4v lw0 = lw[0], lw1 = lw[1], lw2 = lw[2];
             // L as light_vectors computed it for the shadow ray just traced:
             // that ray's direction for a point light, the constant -L for a
             // directional one (q.d is not modified by a trace)
-            V3 L = lt.w == 0.0f ? V3{lt.L[0], lt.L[1], lt.L[2]} : q.d;
+            V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
             const ObjK &ob = p.objs[h.obj];
             // H only feeds the specular power: rsqrt instead of 3 IEEE
             // divisions (<= 2 ulp; vnorm(0) = NaN either way)
@@ -1004,7 +1096,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             V3 H = vmul(hv, __builtin_amdgcn_rsqf(vdot(hv, hv)));
             C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
             C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
-            C3 lc = {lt.col[0], lt.col[1], lt.col[2]};
+            C3 lc = {lw1.x, lw1.y, lw1.z};
             h.acc = cadd(h.acc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
             h.meta += 1u << 9;                       // next light
             if (light + 1 < p.nl) {
@@ -1247,7 +1339,18 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         w_known += (unsigned)__popcll(__ballot(known));
         if (MODE == MODE_BVH) {
-            q.bf = search && (q.skipchk || (!q.closest && q.unb && p.dir_bf));
+            // dir_bf == 1: directional shadow rays go to the scan (a light's
+            // shadow-region tree could not be built)
+            q.bf = search && !q.closest && q.unb && p.dir_bf == 1;
+            // SKIP_TRANS check (main.cpp:997-1002): the stack top's own
+            // nearest root first, then an any-hit search for a candidate the
+            // reference's in-order scan would have taken before it
+            const bool skip = search && q.skipchk;
+            if (skip) {
+                q.tmax = own_nearest(q, p, q.back, cnt);
+                q.closest = false;
+                q.unb = true;
+            }
 #if RT_PROF
             unsigned long long c1 = __builtin_amdgcn_s_memtime();
             pc_shade += c1 - c0;
@@ -1255,7 +1358,29 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(search && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (search && !q.bf) bvh_trace(q, p, stk, cnt);
+            if (search && !q.bf) bvh_trace<false>(q, p, stk, cnt);
+            if (skip) {
+                q.closest = true;
+                q.unb = false;
+                if (!q.skipped) q.win = q.tmax < kFltMax ? q.back : -1;
+            }
+            // directional shadow rays against spheres: a point query in the
+            // light's shadow-region tree (the pass above tested the faces),
+            // unless the faces already made the mask 0 for good
+            if (p.dir_bf == 2) {
+                const bool pt = search && !q.closest && q.unb && !q.bf &&
+                                !(p.shadow_early_out && (q.mask.r == 0.0f) & (q.mask.g == 0.0f) & (q.mask.b == 0.0f));
+                if (__ballot(pt) && pt) {
+                    const DirK &dk = p.dirk[h_light_lds()];
+                    const int root = dk.root;
+                    if (root >= 0) {
+                        V3 po = {fmaf(dk.R[0], q.o.x, fmaf(dk.R[1], q.o.y, dk.R[2] * q.o.z)),
+                                 fmaf(dk.R[3], q.o.x, fmaf(dk.R[4], q.o.y, dk.R[5] * q.o.z)),
+                                 fmaf(dk.R[6], q.o.x, fmaf(dk.R[7], q.o.y, dk.R[8] * q.o.z))};
+                        bvh_trace<true>(q, p, stk, cnt, root, po, dk.cone_k, dk.cone_h);
+                    }
+                }
+            }
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
@@ -1317,6 +1442,21 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #endif
 }
 
+// Gathered row sets -> image order (rt_deinterleave_rows): one thread per
+// float4 of an image row; image row y belongs to rank (y / block) % world as
+// its local row (y / (block * world)) * block + y % block.
+__global__ void deinterleave_kernel(const float *__restrict__ gathered, int world, int rows_per, int W, int H,
+                                    int block, float *__restrict__ image) {
+    const int y = blockIdx.y;
+    const int rank = (y / block) % world;
+    const int k = (y / (block * world)) * block + y % block;
+    const size_t n = (size_t)W * 3;
+    const float *src = gathered + ((size_t)rank * rows_per + k) * n;
+    float *dst = image + (size_t)y * n;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 }  // namespace rt
 
 // ===========================================================================
@@ -1373,8 +1513,11 @@ struct rt_scene {
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
     float4 *d_leafrec = nullptr;
+    DirK *d_dirk = nullptr;            // per light: shadow-region tree (directional lights)
     std::vector<float4> h_fscan, h_sscan;   // host copies for the leaf records
     std::vector<float> h_ofac;
+    std::vector<LightK> h_lights;
+
     int bvh_depth = 0;
     int bvh_stack = 0;
     bool bvh_ok = false;
@@ -1402,6 +1545,24 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
 }
 
 V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
+
+// Textures in their device layout: RGB in a 32-bit word per texel, 8x8-texel
+// tiles row by row (texel_rgb), appended to `words`.
+void tile_texture(const rt_texture_desc &T, TexK &k, std::vector<unsigned> &words) {
+    k.w = T.width;
+    k.h = T.height;
+    k.tiles_x = (T.width + 7) / 8;
+    k.pad = 0;
+    k.off = (long long)words.size();
+    const int tiles_y = (T.height + 7) / 8;
+    words.resize(words.size() + (size_t)k.tiles_x * tiles_y * 64, 0u);
+    for (int y = 0; y < T.height; y++)
+        for (int x = 0; x < T.width; x++) {
+            const unsigned char *c = T.rgb + ((size_t)y * T.width + x) * 3;
+            size_t tile = (size_t)(y >> 3) * k.tiles_x + (x >> 3);
+            words[k.off + tile * 64 + ((y & 7) << 3) + (x & 7)] = c[0] | (c[1] << 8) | ((unsigned)c[2] << 16);
+        }
+}
 
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     size_t shade = (size_t)kLdsHot * kBlock * sizeof(float);         // per-lane shading state
@@ -1466,6 +1627,120 @@ double distance_bound(const rt_scene *s, const float eye[3]) {
         mag = std::max(mag, std::fabs((double)eye[k]));
     }
     return std::max(std::sqrt(diag2), std::sqrt(far2)) + mag + 1.0;
+}
+
+// Shadow-cone tree of a directional light (Params::dirk, dir_bf == 2).
+//
+// The reference's directional shadow ray runs TraceRay with the light's
+// UNNORMALISED direction d = -dir (main.cpp:895), and the sphere test
+// assumes |d| = 1 (main.cpp:1225-1258).  With s = |d|, n = d / s, k = s^2 - 1,
+// h = n.(c - o) (how far the centre is ahead of the origin along the ray) and
+// l = the lateral distance of c from the ray's line, the discriminant is
+//     det / 4 = (d.w)^2 - |w|^2 + r^2 = k h^2 - l^2 + r^2,
+// and the sphere shadows o iff det >= 0 and its far root (-B + sqrt det) / 2
+// exceeds epsilon: for h < 0 that needs o inside the sphere; for h >= 0 it is
+// l^2 <= r^2 + k h^2 -- a cylinder (s = 1), a cone widening away from the
+// light (s > 1) or a bounded cap (s < 1).  It is NOT a ray-geometry
+// question, so the ray BVH cannot cull it.  Here the spheres get a tree of
+// their own, built in the frame whose z axis is n (rows of R: u1, u2, n) over
+// boxes c' +- r_e, and a shadow ray becomes a cone query from R o (device:
+// bvh_trace<true>): a child is entered iff its top is not below the origin
+// (tz >= 0), its lateral distance d from the origin satisfies
+// d^2 <= max(0, k) tz^2, and for s < 1 its bottom is within
+// r_e / sqrt(1 - s^2).  Every candidate is then tested with the exact
+// reference arithmetic; the tree only decides which spheres are tested.
+// Conservative margins: the computed discriminant's error, up to ~2^-21
+// (1 + s^2) D^2, grows r^2 by 2^-18 (1 + s^2) D^2 (r_e), boxes grow by 2^-16 D,
+// k is rounded up.  Returns false if the direction or the geometry is not
+// finite, or the scene is so large that one ulp of B reaches epsilon (then
+// the h < 0 side is no longer safe): the caller falls back to the scan.
+bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4Q> &nodes, std::vector<float4> &rec,
+              DirK &out) {
+    for (int k = 0; k < 9; k++) out.R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+    out.root = -1;
+    out.cone_k = 0.0f;
+    out.cone_h = INFINITY;
+    const double dx = lt.sdir[0], dy = lt.sdir[1], dz = lt.sdir[2];
+    const double sl = std::sqrt(dx * dx + dy * dy + dz * dz);
+    if (!std::isfinite(sl) || !(sl > 0.0)) return false;
+    if (std::ldexp(2.0 * sl * D, -23) >= 0.5 * (double)s->base.eps) return false;
+    const double n[3] = {dx / sl, dy / sl, dz / sl};
+    // u1 perpendicular to n (cross with the axis least aligned with n), u2 = n x u1
+    int ax = 0;
+    for (int k = 1; k < 3; k++)
+        if (std::fabs(n[k]) < std::fabs(n[ax])) ax = k;
+    double e[3] = {0, 0, 0};
+    e[ax] = 1.0;
+    double u1[3] = {n[1] * e[2] - n[2] * e[1], n[2] * e[0] - n[0] * e[2], n[0] * e[1] - n[1] * e[0]};
+    const double l1 = std::sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
+    for (double &v : u1) v /= l1;
+    const double u2[3] = {n[1] * u1[2] - n[2] * u1[1], n[2] * u1[0] - n[0] * u1[2], n[0] * u1[1] - n[1] * u1[0]};
+    for (int k = 0; k < 3; k++) {
+        out.R[k] = (float)u1[k];
+        out.R[3 + k] = (float)u2[k];
+        out.R[6 + k] = (float)n[k];
+    }
+    // the device rotates with the float R: boxes are computed with it too
+    // (its rounding of R o, ~2^-22 D, is far inside the 2^-16 D margins)
+    double R[9];
+    for (int k = 0; k < 9; k++) R[k] = out.R[k];
+    const double pad = std::ldexp(D, -16);
+    const double s2 = sl * sl;
+    std::vector<rtbvh::Prim> P;
+    double re_max = 0.0;
+    for (const auto &src : s->prims) {
+        if (!src.sphere) continue;
+        const double c[3] = {src.c[0], src.c[1], src.c[2]};
+        const double r = std::fabs((double)src.r);
+        if (!std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]) || !std::isfinite(r)) return false;
+        const double re = std::sqrt(r * r + std::ldexp((1.0 + s2) * D * D, -18)) + 2.0 * pad;
+        re_max = std::max(re_max, re);
+        rtbvh::Prim q;
+        q.key = src.key;
+        q.cost = 1.0f;
+        for (int k = 0; k < 3; k++) {
+            const double cr = R[3 * k] * c[0] + R[3 * k + 1] * c[1] + R[3 * k + 2] * c[2];
+            q.box.lo[k] = std::nextafter((float)(cr - re), -INFINITY);
+            q.box.hi[k] = std::nextafter((float)(cr + re), INFINITY);
+            q.c[k] = (float)cr;
+        }
+        P.push_back(q);
+    }
+    if (P.empty()) return true;                          // root -1: no sphere can shadow
+    out.cone_k = std::nextafter((float)(std::max(0.0, s2 - 1.0) * (1.0 + std::ldexp(1.0, -16))), INFINITY);
+    if (s2 < 1.0) out.cone_h = std::nextafter((float)(re_max / std::sqrt(1.0 - s2) + pad), INFINITY);
+    rtbvh::Result Rb;
+    rtbvh::Builder B(P);
+    B.max_leaf = (int)s->opt_bvh_leaf;
+    B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
+    if (!B.build(Rb) || Rb.nodes.empty()) return false;
+    rtbvh::Result4 Q;
+    rtbvh::collapse<4>(Rb, Q);
+    rtbvh::bfs_order(Q);
+    if (Q.max_stack > kStack) return false;
+    const int nf = s->base.nf;
+    bool ok = rtbvh::leaf_records(
+        Q, Rb.keys, [](int32_t) { return false; },
+        [&](int32_t k) {
+            float kb;
+            memcpy(&kb, &k, sizeof kb);
+            rec.push_back(s->h_sscan[k - nf]);
+            rec.push_back(make_float4(kb, s->h_ofac[k], 0.0f, 0.0f));
+            return 2;
+        },
+        rec.size());
+    std::vector<rtbvh::Node4Q> QQ;
+    if (!ok || !rtbvh::quantize(Q, QQ)) return false;
+    const int base = (int)nodes.size();
+    for (auto &z : QQ) {
+        for (auto &l : z.link) {
+            if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
+            else if (l >= 0) l += base;
+        }
+        nodes.push_back(z);
+    }
+    out.root = base;
+    return true;
 }
 
 // (Re)build the BVH with boxes padded for distance bound D (see rt_bvh.h):
@@ -1543,35 +1818,60 @@ int build_bvh(rt_scene *s, double D) {
             if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
     // the device stack holds kStack entries: a deeper tree uses the scan
     ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
+    // directional lights in a scene with spheres: shadow-region trees, after
+    // the main tree in the same node and record arrays
+    std::vector<DirK> dirk(s->h_lights.size());
+    int dir_mode = 0;
+    if (ok && s->base.ns > 0) {
+        rec.resize(rec.size() - 3);                  // the 3 padding words go after the last tree
+        for (size_t l = 0; l < s->h_lights.size(); l++) {
+            if (s->h_lights[l].w != 0.0f) continue;
+            if (dir_mode == 0) dir_mode = 2;
+            if (!dir_tree(s, s->h_lights[l], D, QQ, rec, dirk[l])) dir_mode = 1;
+        }
+        rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        if ((rec.size() >> 8) >= (1u << 23) - 2) ok = false;
+    }
     // The old tree stays valid until the new one is on the device: upload into
     // new buffers first, then swap (a failed rebuild leaves no dangling
     // pointers and no tree marked valid that is not there).
     float4 *nb = nullptr, *nr = nullptr;
+    DirK *nd = nullptr;
     int rc = RT_OK;
     if (ok) {
         const size_t node_bytes = QQ.size() * sizeof(QQ[0]);
+        const size_t dir_bytes = std::max<size_t>(1, dirk.size()) * sizeof(DirK);
         if (hipMalloc(&nb, node_bytes) != hipSuccess ||
-            hipMalloc(&nr, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess)
+            hipMalloc(&nr, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&nd, dir_bytes) != hipSuccess)
             rc = RT_E_NOMEM;
         else if (hipMemcpy(nb, QQ.data(), node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
-                 hipMemcpy(nr, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess)
+                 hipMemcpy(nr, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess ||
+                 (!dirk.empty() && hipMemcpy(nd, dirk.data(), dirk.size() * sizeof(DirK), hipMemcpyHostToDevice) !=
+                                       hipSuccess))
             rc = RT_E_HIP;
         if (rc) {
             if (nb) (void)hipFree(nb);
             if (nr) (void)hipFree(nr);
+            if (nd) (void)hipFree(nd);
             nb = nr = nullptr;
+            nd = nullptr;
         }
     }
     // renders still queued may read the old tree: free it after they finish
-    if (s->d_bvh || s->d_leafrec) {
+    if (s->d_bvh || s->d_leafrec || s->d_dirk) {
         (void)hipDeviceSynchronize();
         if (s->d_bvh) (void)hipFree(s->d_bvh);
         if (s->d_leafrec) (void)hipFree(s->d_leafrec);
+        if (s->d_dirk) (void)hipFree(s->d_dirk);
     }
     s->d_bvh = nb;
     s->d_leafrec = nr;
+    s->d_dirk = nd;
     s->base.bvh = nb;
     s->base.leafrec = nr;
+    s->base.dirk = nd;
+    s->base.dir_bf = dir_mode;
     s->bvh_ok = ok && rc == RT_OK;
     s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
     s->bvh_depth = s->bvh_ok ? Q.depth : 0;
@@ -1597,6 +1897,8 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
             mode = MODE_BVH;
             p.bvh = s->base.bvh;
             p.leafrec = s->base.leafrec;
+            p.dirk = s->base.dirk;
+            p.dir_bf = s->base.dir_bf;
             p.bvh_stack = std::max(1, s->bvh_stack);
         }
     }
@@ -1783,6 +2085,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     s->h_fscan = fscan;
     s->h_sscan = sscan;
     s->h_ofac = ofac;
+    s->h_lights.clear();
     std::vector<LightK> lights((size_t)desc->n_lights);
     for (int i = 0; i < desc->n_lights; i++) {
         const rt_light_desc &L = desc->lights[i];
@@ -1796,13 +2099,8 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
         k.L[0] = Ld.x, k.L[1] = Ld.y, k.L[2] = Ld.z;
         k.sdir[0] = sd.x, k.sdir[1] = sd.y, k.sdir[2] = sd.z;
     }
+    s->h_lights = lights;
     std::vector<TexK> texs((size_t)desc->n_textures);
-    std::vector<unsigned char> texels;
-    for (int i = 0; i < desc->n_textures; i++) {
-        const rt_texture_desc &T = desc->textures[i];
-        texs[i].w = T.width, texs[i].h = T.height, texs[i].off = (long long)texels.size();
-        texels.insert(texels.end(), T.rgb, T.rgb + (size_t)T.width * T.height * 3);
-    }
 
     int rc = RT_OK;
     Params &p = s->base;
@@ -1812,6 +2110,8 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     if (!rc) rc = upload(s, objs, p.objs);
     if (!rc) rc = upload(s, fsh, p.fsh);
     if (!rc) rc = upload(s, lights, p.lights);
+    std::vector<unsigned> texels;
+    for (int i = 0; i < desc->n_textures; i++) tile_texture(desc->textures[i], texs[i], texels);
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
     if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
@@ -1835,9 +2135,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.eta_bkg = desc->eta_bkg;
     p.eps = desc->epsilon;
     p.depth = desc->depth;
-    p.dir_bf = 0;
-    for (int i = 0; i < desc->n_lights; i++)
-        if (desc->lights[i].w == 0.0f && ns > 0) p.dir_bf = 1;
+    p.dir_bf = 0;                      // set with the BVH (build_bvh); the scan needs none
     p.shadow_early_out = nan_fac ? 0 : 1;
     p.stack_cap = kLdsStackDefault;
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
@@ -1852,8 +2150,10 @@ int rt_scene_destroy(rt_scene *s) {
     for (auto &r : s->slots)           // renders still running on caller or slot streams
         if (r.ev1) (void)hipEventSynchronize(r.ev1);
     for (void *d : s->allocs) (void)hipFree(d);
+
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_leafrec) (void)hipFree(s->d_leafrec);
+    if (s->d_dirk) (void)hipFree(s->d_dirk);
     if (s->dev_out) (void)hipFree(s->dev_out);
     for (auto &r : s->slots) free_slot(r);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1933,6 +2233,23 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
     if (slot.stream && hipStreamWaitEvent(caller, slot.ev1, 0) != hipSuccess) return RT_E_HIP;
     s->last_valid = rc == RT_OK;
     return rc;
+}
+
+int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
+                         void *hip_stream) {
+    if (!gathered || !image || world < 1 || rows_per < 1 || W < 1 || H < 1 || block < 1) return RT_E_INVALID;
+    if (H > 65535) return RT_E_UNSUPPORTED;
+    // every image row's source row must exist: each rank's row count <= rows_per
+    const int nblocks = (H + block - 1) / block;
+    for (int r = 0; r < world; r++) {
+        int rows = 0;
+        for (int b = r; b < nblocks; b += world) rows += std::min(block, H - b * block);
+        if (rows > rows_per) return RT_E_INVALID;
+    }
+    const unsigned gx = (unsigned)std::min<size_t>(64, ((size_t)W * 3 + 255) / 256);
+    hipLaunchKernelGGL(deinterleave_kernel, dim3(gx, (unsigned)H), dim3(256), 0, (hipStream_t)hip_stream, gathered,
+                       world, rows_per, W, H, block, image);
+    return hipGetLastError() == hipSuccess ? RT_OK : RT_E_HIP;
 }
 
 int rt_scene_prepare(rt_scene *s, const rt_camera *cam, int W, int H) {

@@ -86,11 +86,11 @@ _hip = None
 
 HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_set_imsize",
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
-                "rth_output_path"]
+                "rth_output_path", "rth_row_set"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks",
                "rt_scene_last_stats", "rt_scene_prepare",
-               "rt_scene_set_option", "rt_scene_debug_counters", "rt_strerror"]
+               "rt_scene_set_option", "rt_scene_debug_counters", "rt_deinterleave_rows", "rt_strerror"]
 
 
 def host_lib() -> C.CDLL:
@@ -112,6 +112,7 @@ def host_lib() -> C.CDLL:
         L.rth_quantize.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
         L.rth_write_ppm.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
         L.rth_output_path.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.rth_row_set.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4
         _host = L
     return _host
 
@@ -147,6 +148,8 @@ def hip_lib() -> C.CDLL:
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_prepare.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+        L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                           C.c_void_p]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
         L.rt_strerror.restype = C.c_char_p

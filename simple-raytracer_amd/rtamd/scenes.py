@@ -35,6 +35,15 @@ CONFIGS = {
                lights="dir+point", depth=4),
     "C5": dict(w=16384, h=16384, spheres=100000, tris=0, ks=0.5, glass=0.10, textured=False,
                lights="point2", depth=8),
+    # C3 variants that exercise the reference's order-dependent special cases
+    # (VERDICT r1 "brute-force cliff"): a directional light with an
+    # unnormalised direction in a scene with spheres (main.cpp:895, the sphere
+    # test's A = 1 quirk), and glass triangles (face-incident refraction, the
+    # SKIP_TRANS rule main.cpp:1000-1002)
+    "C3D": dict(w=4096, h=4096, spheres=1000, tris=1000, ks=0.5, glass=0.10, textured=False,
+                lights="dir+point", depth=4),
+    "C3G": dict(w=4096, h=4096, spheres=1000, tris=1000, ks=0.5, glass=0.10, textured=False,
+                lights="point2", depth=4, tri_glass=0.10),
 }
 
 TEXTURE_NAME = "c4_texture.ppm"
@@ -93,7 +102,9 @@ def scene_text(name: str, w: int | None = None, h: int | None = None, seed: int 
                 b = 3 * i
                 out.append(f"f {b+1}/{b+1} {b+2}/{b+2} {b+3}/{b+3}\n")
             else:
-                out.append(mtl(False))
+                # (the draw only happens for configs with glass triangles:
+                # the other configs' random streams stay as they were)
+                out.append(mtl(cfg.get("tri_glass", 0.0) > 0 and rnd.random() < cfg["tri_glass"]))
                 b = 3 * i
                 out.append(f"f {b+1} {b+2} {b+3}\n")
     for i in range(cfg["spheres"]):

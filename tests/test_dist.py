@@ -72,3 +72,25 @@ def test_row_sets_cover_image():
                 assert len(rr) == n and all(0 <= y < H for y in rr)
                 rows += rr
             assert sorted(rows) == list(range(H))
+
+
+@pytest.mark.parametrize("H", [1, 7, 8, 9, 64, 67, 1080, 4096])
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_cli_row_set_matches_dist(H, world):
+    """The C++ CLI's multi-device row mapping (rth_row_set, librt_host) is the
+    one the Python bench uses (rtamd.dist.row_set): every image row exactly
+    once, equal-size gather buffers."""
+    import ctypes as C
+    import rtamd
+    from rtamd.dist import row_set
+    L = rtamd.host_lib()
+    seen = []
+    for r in range(world):
+        y0, step, n, per = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        assert L.rth_row_set(H, world, r, 8, C.byref(y0), C.byref(step), C.byref(n), C.byref(per)) == 0
+        py = row_set(H, world, r)
+        assert (y0.value, 8, step.value, n.value, per.value) == py
+        seen += [y0.value + (k // 8) * step.value + k % 8 for k in range(n.value)]
+    assert sorted(seen) == list(range(H))
+    y = C.c_int()
+    assert L.rth_row_set(H, world, world, 8, C.byref(y), C.byref(y), C.byref(y), C.byref(y)) == -1

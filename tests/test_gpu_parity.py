@@ -7,6 +7,7 @@ import json
 import os
 import shutil
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -501,3 +502,100 @@ def test_bvh_rebuild_on_camera_move():
     eq = lambda x, y: np.array_equal(np.nan_to_num(x, nan=-9), np.nan_to_num(y, nan=-9))
     assert eq(a, fa) and eq(c, fa) and eq(b, fb)
     assert _counts(sa) == _counts(sc)
+
+
+@pytest.mark.parametrize("accel", [0, 1])
+@pytest.mark.parametrize("cfg", ["C3D", "C3G"])
+def test_special_cases_on_the_bvh(cfg, accel, tmp_path):
+    """C3 with a directional light (unnormalised direction against spheres:
+    the reference's A = 1 sphere quirk, main.cpp:895) and C3 with glass
+    triangles (SKIP_TRANS, main.cpp:1000-1002): the BVH answers both exactly
+    -- shadow-region point queries, and the stack top's own root plus an
+    any-hit search -- with no brute-force query left; the scan (accel=0)
+    agrees.  Against the oracle (pinned to the reference by
+    test_float_goldens' C3D/C3G fixtures) with identical ray counts."""
+    name = f"{cfg}_48x40.txt"
+    (tmp_path / name).write_text(gen.scene_text(cfg, w=48, h=40))
+    img, st, ref, cnt = _render_both(name, str(tmp_path), accel=accel)
+    assert_parity(img, ref, f"{cfg} accel{accel}")
+    assert _counts(st) == cnt
+    if accel == 1:
+        assert st.bf_queries == 0
+    if cfg == "C3G":
+        assert cnt["skip_trans"] > 0
+    _summary[f"{cfg}@accel{accel}"] = dict(compare(img, ref), counts=_counts(st), bf=st.bf_queries,
+                                          tests=dict(box=st.box_tests, face=st.face_tests, sphere=st.sphere_tests))
+
+
+def test_deinterleave_rows_device():
+    """rt_deinterleave_rows puts gathered row sets (rth_row_set's dealing)
+    back in image order on the device, for ragged heights and several ranks."""
+    torch = pytest.importorskip("torch")
+    import ctypes as C
+    from rtamd.dist import image_rows, row_set
+    L = rtamd.hip_lib()
+    for H, world in ((67, 3), (8, 2), (130, 8), (5, 1)):
+        W = 13
+        per = row_set(H, world, 0)[4]
+        g = torch.rand((world, per, W, 3), dtype=torch.float32, device="cuda:0")
+        img = torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
+        rc = L.rt_deinterleave_rows(C.c_void_p(g.data_ptr()), world, per, W, H, 8, C.c_void_p(img.data_ptr()),
+                                    C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0
+        torch.cuda.synchronize()
+        want = torch.empty_like(img)
+        for r in range(world):
+            rows = image_rows(H, world, r)
+            if rows:
+                want[rows] = g[r, : len(rows)]
+        assert torch.equal(img, want), (H, world)
+        assert L.rt_deinterleave_rows(C.c_void_p(g.data_ptr()), world, per - 1 if per > 1 else 0, W, H, 8,
+                                      C.c_void_p(img.data_ptr()), None) == -1
+
+
+@pytest.mark.parametrize("name", ["test7_s.txt", "C3_64x64.txt"])
+def test_cli_rccl_gather(name, tmp_path):
+    """`rt --gpus 1 --gather rccl`: the image goes through the multi-device
+    path (row blocks rendered into HBM, ncclGather to the first device, device
+    de-interleave, one copy to the host) and equals the single-call render
+    bit for bit (float buffer and PPM)."""
+    outs = {}
+    for mode in ("host", "rccl"):
+        tmp_name = f"_cli_{mode}_" + name
+        shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
+        ppm = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
+        fout = str(tmp_path / f"{mode}.bin")
+        try:
+            r = subprocess.run([CLI, tmp_name, "--gpus", "1", "--gather", mode, "--float-out", fout, "--stats"],
+                               cwd=SCENES, capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            outs[mode] = (open(ppm, "rb").read(), np.fromfile(fout, dtype=np.float32), r.stderr)
+        finally:
+            for p in (os.path.join(SCENES, tmp_name), ppm):
+                if os.path.exists(p):
+                    os.remove(p)
+    assert outs["host"][0] == outs["rccl"][0]
+    a, b = outs["host"][1], outs["rccl"][1]
+    assert np.array_equal(np.nan_to_num(a, nan=-9), np.nan_to_num(b, nan=-9))
+    assert "rays primary=" in outs["rccl"][2]
+
+
+def test_multi_rank_hip_path_gloo():
+    """The N > 1 bench data path with the HIP renderer (not the oracle): two
+    ranks on one GPU (gloo gather staged through the host), each rendering
+    its interleaved row set; rank 0 checks the gathered image bit for bit
+    against one whole-image render (bench.py --verify)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--verify", "--steps", "2", "--warmup", "1",
+           "--config", "C2", "--cpu-baseline", "off"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["verified"] is True and line["n_gpus"] == 2
+    _summary["multi_rank_gloo_C2"] = dict(value=line["value"], verified=line["verified"])

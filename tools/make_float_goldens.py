@@ -134,19 +134,28 @@ def main() -> None:
     c5 = os.path.join(work, "C5_12x12.txt")
     open(c5, "w").write(gen.scene_text("C5", w=12, h=12))
     jobs.append(("C5_12x12@d8", c5, work, 8))
+    # C3 variants with a directional light (unnormalised direction, spheres)
+    # and with glass triangles (SKIP_TRANS), at 64x64
+    gen_specs = {"C5_12x12@d8": ("C5", 12, 12)}
+    for cfg in ("C3D", "C3G"):
+        path = os.path.join(work, f"{cfg}_64x64.txt")
+        open(path, "w").write(gen.scene_text(cfg, w=64, h=64))
+        jobs.append((f"{cfg}_64x64", path, work, None))
+        gen_specs[f"{cfg}_64x64"] = (cfg, 64, 64)
     index = {}
     for fix, scene, cwd, depth in jobs:
         path = scene if os.path.isabs(scene) else os.path.join(cwd, scene)
         f, md5, cnt = run(exe, path, cwd, depth, work)
         base = os.path.basename(scene)
-        if depth is None:
+        if depth is None and base in gold:
             assert md5 == gold[base]["md5"], f"{fix}: instrumented build changed the output"
             assert sum(cnt.values()) == gold[base]["trace_calls"], (fix, cnt)
         np.savez_compressed(os.path.join(OUT, fix + ".npz"), f=f)
         index[fix] = dict(scene=base, depth=4 if depth is None else depth, width=f.shape[1],
                           height=f.shape[0], md5=md5, counts=cnt, nan_px=int(np.isnan(f).any(-1).sum()))
-        if base.startswith("C5_12x12"):
-            index[fix]["generated"] = {"config": "C5", "w": 12, "h": 12}
+        if fix in gen_specs:
+            c, w, h = gen_specs[fix]
+            index[fix]["generated"] = {"config": c, "w": w, "h": h}
         print(f"{fix:32s} {f.shape[1]}x{f.shape[0]} d={index[fix]['depth']} {cnt}", flush=True)
     with open(os.path.join(OUT, "index.json"), "w") as fh:
         json.dump(index, fh, indent=1, sort_keys=True)
