@@ -121,9 +121,7 @@ struct LightK {
 };
 struct TexK {
     int w, h;
-    int tiles_x;                         // 8x8-texel tiles per tile row
-    int pad;
-    long long off;                       // first texel word in Params::texels
+    long long off;                       // first byte in Params::texels
 };
 // directional light: its shadow-region tree over the spheres (rt host:
 // dir_trees) -- root node in Params::bvh (-1: no sphere can shadow) and the
@@ -142,7 +140,7 @@ struct Params {
     const ObjK *__restrict__ objs;
     const FaceShadeK *__restrict__ fsh;
     const LightK *__restrict__ lights;
-    const unsigned *__restrict__ texels; // all textures: RGBA8 words in 8x8-texel tiles
+    const unsigned char *__restrict__ texels;   // all textures: RGB bytes, row-major
     const TexK *__restrict__ texs;
     float *__restrict__ out;
     unsigned int *__restrict__ work;     // pixel work counter
@@ -789,22 +787,14 @@ __device__ void hit_geometry(const Params &p, int obj, V3 o, V3 d, float t, V3 &
     }
 }
 
-// Texel (x, y) of a texture -- the reference's nearest texel (main.cpp:816-818,
-// :850-852).  Textures live in HBM as one 32-bit word per texel (R, G, B
-// bytes) in 8x8-texel tiles (256 B, two cache lines): one load per texel
-// instead of three byte loads, and neighbouring texels -- what neighbouring
-// pixels fetch -- share lines in both directions.  (gfx950 exposes no image
-// arrays through HIP -- hipMallocArray: "operation not supported",
-// tools/tex_probe.hip -- so the texture unit's tiled image path is not
-// available; this is its layout in a plain buffer.)  Each channel then goes
-// through the reference's map(v, 0, 255, 0, 1) in float.
-__device__ __forceinline__ float tex_map(unsigned v) {
-    return ((float)v - 0.0f) * (1.0f - 0.0f) / (255.0f - 0.0f) + 0.0f;
-}
-__device__ __forceinline__ C3 texel_rgb(const Params &p, const TexK &t, int x, int y) {
-    const long long tile = (long long)(y >> 3) * t.tiles_x + (x >> 3);
-    const unsigned w = p.texels[t.off + tile * 64 + ((y & 7) << 3) + (x & 7)];
-    return C3{tex_map(w & 0xffu), tex_map((w >> 8) & 0xffu), tex_map((w >> 16) & 0xffu)};
+// Texel (x, y) of a texture, channel c -- the reference's nearest texel
+// (main.cpp:816-818, :850-852) through map(v, 0, 255, 0, 1) in float.
+// Textures are RGB bytes, row-major, in HBM (gfx950 exposes
+// no image arrays through HIP, and 32-bit texels in 8x8 tiles measured no
+// faster on C4).
+__device__ __forceinline__ float texel(const Params &p, const TexK &t, int x, int y, int c) {
+    float v = (float)p.texels[t.off + ((long long)y * t.w + x) * 3 + c];
+    return (v - 0.0f) * (1.0f - 0.0f) / (255.0f - 0.0f) + 0.0f;   // map(v, 0, 255, 0, 1)
 }
 
 // ShadeRay prologue (main.cpp:785-872): hit record, diffuse / texture and the
@@ -891,7 +881,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
                                 (float)((double)height - 1.0));
             int j = (int)clampr((float)round(((double)width - 1.0) * (double)u), 0.0f,
                                 (float)((double)width - 1.0));
-            dif = texel_rgb(p, tx, j, i);
+            dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
         } else {                                                     // main.cpp:834-861
             const FaceShadeK &fs = p.fsh[obj];
             float u = (bary.x * fs.vt[0][0]) + (bary.y * fs.vt[1][0]) + (bary.z * fs.vt[2][0]);
@@ -900,7 +890,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
             u = clampr(u, 0.0f, 1.0f);
             int i = (int)clampr(roundf((width - 1.0f) * u), 0.0f, (float)((double)width - 1.0));
             int j = (int)clampr(roundf((height - 1.0f) * v), 0.0f, (float)((double)height - 1.0));
-            dif = texel_rgb(p, tx, i, j);
+            dif = {texel(p, tx, i, j, 0), texel(p, tx, i, j, 1), texel(p, tx, i, j, 2)};
         }
     }
     if ((double)cosI < 0.0 && ob.is_sphere) {                      // main.cpp:869-872
@@ -1500,6 +1490,7 @@ struct rt_scene {
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
     long long opt_bvh_leaf = 8;        // SAH max leaf size
     long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
+    long long opt_fail_bvh_upload = 0; // test hook: the next BVH uploads fail (RT_E_NOMEM)
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
     struct PrimSrc {
         int key;
@@ -1545,24 +1536,6 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
 }
 
 V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
-
-// Textures in their device layout: RGB in a 32-bit word per texel, 8x8-texel
-// tiles row by row (texel_rgb), appended to `words`.
-void tile_texture(const rt_texture_desc &T, TexK &k, std::vector<unsigned> &words) {
-    k.w = T.width;
-    k.h = T.height;
-    k.tiles_x = (T.width + 7) / 8;
-    k.pad = 0;
-    k.off = (long long)words.size();
-    const int tiles_y = (T.height + 7) / 8;
-    words.resize(words.size() + (size_t)k.tiles_x * tiles_y * 64, 0u);
-    for (int y = 0; y < T.height; y++)
-        for (int x = 0; x < T.width; x++) {
-            const unsigned char *c = T.rgb + ((size_t)y * T.width + x) * 3;
-            size_t tile = (size_t)(y >> 3) * k.tiles_x + (x >> 3);
-            words[k.off + tile * 64 + ((y & 7) << 3) + (x & 7)] = c[0] | (c[1] << 8) | ((unsigned)c[2] << 16);
-        }
-}
 
 size_t mode_lds_bytes(const rt_scene *s, int mode) {
     size_t shade = (size_t)kLdsHot * kBlock * sizeof(float);         // per-lane shading state
@@ -1838,6 +1811,10 @@ int build_bvh(rt_scene *s, double D) {
     float4 *nb = nullptr, *nr = nullptr;
     DirK *nd = nullptr;
     int rc = RT_OK;
+    if (ok && s->opt_fail_bvh_upload) {        // test hook: as if the device allocation failed
+        rc = RT_E_NOMEM;
+        ok = false;
+    }
     if (ok) {
         const size_t node_bytes = QQ.size() * sizeof(QQ[0]);
         const size_t dir_bytes = std::max<size_t>(1, dirk.size()) * sizeof(DirK);
@@ -2110,8 +2087,12 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     if (!rc) rc = upload(s, objs, p.objs);
     if (!rc) rc = upload(s, fsh, p.fsh);
     if (!rc) rc = upload(s, lights, p.lights);
-    std::vector<unsigned> texels;
-    for (int i = 0; i < desc->n_textures; i++) tile_texture(desc->textures[i], texs[i], texels);
+    std::vector<unsigned char> texels;
+    for (int i = 0; i < desc->n_textures; i++) {
+        const rt_texture_desc &T = desc->textures[i];
+        texs[i].w = T.width, texs[i].h = T.height, texs[i].off = (long long)texels.size();
+        texels.insert(texels.end(), T.rgb, T.rgb + (size_t)T.width * T.height * 3);
+    }
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
     if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
@@ -2170,6 +2151,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "depth") s->base.depth = (int)value;
     else if (k == "accel") s->opt_accel = value;
     else if (k == "inflight") return set_inflight(s, value);
+    else if (k == "fail_bvh_upload") s->opt_fail_bvh_upload = value;
     else if (k == "lds_stack") {
         if (value < 12 || value > kLdsStack) return RT_E_INVALID;
         s->base.stack_cap = (int)value;

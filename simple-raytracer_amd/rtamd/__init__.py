@@ -112,7 +112,8 @@ def host_lib() -> C.CDLL:
         L.rth_quantize.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
         L.rth_write_ppm.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
         L.rth_output_path.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
-        L.rth_row_set.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4
+        if hasattr(L, "rth_row_set"):     # absent from round-1 libraries (A/B baselines)
+            L.rth_row_set.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4
         _host = L
     return _host
 
@@ -148,8 +149,9 @@ def hip_lib() -> C.CDLL:
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_prepare.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
-        L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
-                                           C.c_void_p]
+        if hasattr(L, "rt_deinterleave_rows"):
+            L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                               C.c_void_p, C.c_void_p]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
         L.rt_strerror.restype = C.c_char_p

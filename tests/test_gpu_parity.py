@@ -599,3 +599,24 @@ def test_multi_rank_hip_path_gloo():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["verified"] is True and line["n_gpus"] == 2
     _summary["multi_rank_gloo_C2"] = dict(value=line["value"], verified=line["verified"])
+
+
+def test_bvh_upload_failure_leaves_no_stale_tree():
+    """A BVH rebuild whose device upload fails returns RT_E_NOMEM and leaves
+    no tree marked valid (the old one is freed, nothing dangles); the next
+    render rebuilds and is identical to a fresh scene's."""
+    hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
+    W, H = hs.width, hs.height
+    cam = hs.camera()
+    gs = rtamd.GpuScene(hs)
+    a, _ = gs.render_rows(cam, W, H, 0, H)
+    gs.set_option("fail_bvh_upload", 1)
+    gs.set_option("bvh_leaf", 8)                  # forces a rebuild at the next render
+    with pytest.raises(rtamd.RTError):
+        gs.render_rows(cam, W, H, 0, H)
+    with pytest.raises(rtamd.RTError):            # still failing: retried, not a stale tree
+        gs.render_rows(cam, W, H, 0, H)
+    gs.set_option("fail_bvh_upload", 0)
+    b, sb = gs.render_rows(cam, W, H, 0, H)
+    assert np.array_equal(np.nan_to_num(a, nan=-9), np.nan_to_num(b, nan=-9))
+    assert gs.debug_counters()[16] == 2           # BVH mode again
