@@ -1,2 +1,3 @@
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out && \
-timeout -k 10 900 python tools/ab.py --rounds 3 --steps 20 cur: pk:lib_pk > gpurun_out/ab_pk.log 2>&1; echo "ab rc=$?"; tail -4 gpurun_out/ab_pk.log
+for c in C2 C5; do s=20; [ $c = C5 ] && s=4; timeout -k 10 600 python bench.py --config $c --cpu-baseline off --steps $s --warmup 1 > gpurun_out/bench_$c.log 2>&1; echo "bench $c rc=$?"; python -c "
+import json; j=json.loads(open('gpurun_out/bench_$c.log').read().strip().splitlines()[-1]); print('$c', j['value'], j['ms_per_step'], j['work'], j['config']['launch'], j['one_frame'])"; done
