@@ -1093,7 +1093,12 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 // next light's shadow ray from the same point: origin, self
                 // and cumulative mask are already in q (main.cpp:885-928)
                 lds_store_light(h);
-                shadow_query(q, p, light + 1, h.obj);
+                // (opaque index: reusing this light's address for the next
+                // one kept a 64-bit pointer live -- and spilled -- across the
+                // shading code)
+                int next = light + 1;
+                asm volatile("" : "+v"(next));
+                shadow_query(q, p, next, h.obj);
                 ls.top = top;
                 return RK_SHADOW;
             }
