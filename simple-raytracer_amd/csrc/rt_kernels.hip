@@ -346,6 +346,10 @@ __device__ __forceinline__ float own_nearest(const Query &q, const Params &p, in
 
 
 constexpr int kNodeF4 = 4;                       // float4 per quantised 4-wide node (rt_bvh.h Node4Q)
+// while-while traversal: stop descending when at most this many lanes still
+// look for a leaf (A/B, C3 Mrays/s: 0 -> 5912, 1 -> 5960, 2 -> 5957, 3 -> 5954,
+// 6 -> 5924, 12 -> 5849; profiles/r02/ab_leaf_threshold.txt)
+constexpr unsigned kLeafWait = 2;
 constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
 constexpr int kNStats = 40;                      // device counter slots (rt_scene_debug_counters)
 
@@ -420,8 +424,8 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 //
 // While-while traversal with speculative leaf postponement (Aila & Laine
 // 2009): a lane that reaches a leaf parks it and keeps descending inner nodes
-// until every active lane of the wave holds a leaf; the leaves are then
-// visited together.  Node visits stay one dependent fetch each, and the leaf
+// until all but kLeafWait active lanes of the wave hold a leaf; the leaves are
+// then visited together.  Node visits stay one dependent fetch each, and the leaf
 // code runs with most lanes active instead of in almost every wave trip (+6 %
 // over an if-if loop).  The result does not depend on the visiting order.
 //
@@ -602,7 +606,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
-            if (__ballot(leaf == rtbvh::kEmpty) == 0ull) break;   // every lane holds a leaf
+            // all but kLeafWait lanes hold a leaf: visit the leaves now (the
+            // few still descending wait one leaf round)
+            if ((unsigned)__popcll(__ballot(leaf == rtbvh::kEmpty)) <= kLeafWait) break;
         }
         // visit the parked leaf, then any leaf the lane stopped on
         while (leaf != rtbvh::kEmpty) {
