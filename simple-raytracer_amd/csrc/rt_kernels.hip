@@ -348,7 +348,8 @@ __device__ __forceinline__ float own_nearest(const Query &q, const Params &p, in
 constexpr int kNodeF4 = 4;                       // float4 per quantised 4-wide node (rt_bvh.h Node4Q)
 // while-while traversal: stop descending when at most this many lanes still
 // look for a leaf (A/B, C3 Mrays/s: 0 -> 5912, 1 -> 5960, 2 -> 5957, 3 -> 5954,
-// 6 -> 5924, 12 -> 5849; profiles/r02/ab_leaf_threshold.txt)
+// 6 -> 5924, 12 -> 5849; with one leaf per round: 0 -> 5885, 2 -> 6021,
+// 5 -> 6031; profiles/r02/ab_leaf_*.txt)
 constexpr unsigned kLeafWait = 2;
 constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
 constexpr int kNStats = 40;                      // device counter slots (rt_scene_debug_counters)
@@ -610,8 +611,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
             // few still descending wait one leaf round)
             if ((unsigned)__popcll(__ballot(leaf == rtbvh::kEmpty)) <= kLeafWait) break;
         }
-        // visit the parked leaf, then any leaf the lane stopped on
-        while (leaf != rtbvh::kEmpty) {
+        // visit the parked leaf; a leaf the lane stopped on is parked for the
+        // next round (one leaf per lane per round: +0.8 % over visiting them
+        // back to back, profiles/r02/ab_leaf_one_per_round.txt)
+        if (leaf != rtbvh::kEmpty) {
 #if RT_PROF
             cnt.trips++;
 #endif
@@ -627,7 +630,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
                 node = pop();
             }
         }
-        if (node == rtbvh::kEmpty) break;
+        if (node == rtbvh::kEmpty && leaf == rtbvh::kEmpty) break;
     }
     if (q.closest) {
         if (win >= 0) {
