@@ -193,8 +193,10 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * stream by events: renders issued on different caller streams -- independent
  * frames -- overlap, so one frame's tail is filled by the next frame's work),
  * "lds_stack" (12..16, default 14: BVH stack entries kept in LDS per lane;
- * deeper stacks spill to device memory -- a test knob), "fail_bvh_upload"
- * (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
+ * deeper stacks spill to device memory -- a test knob), "bvh_leaf",
+ * "bvh_trav" (binary SAH: largest leaf, node cost x1000), "bvh_collapse"
+ * (0 greedy, 1 SAH-optimal 4-wide collapse), "bvh_node" (its node cost x1000),
+ * "fail_bvh_upload" (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
 /* Raw counters of the last render (diagnostics): [0..8] as in rt_stats,

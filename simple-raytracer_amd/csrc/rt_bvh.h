@@ -63,6 +63,7 @@ struct Prim {
 struct Result {
     std::vector<Node> nodes;
     std::vector<int32_t> keys;   // leaf-ordered object indices
+    std::vector<float> costs;    // their Prim::cost
     int depth = 0;
 };
 
@@ -158,52 +159,220 @@ inline void collapse(const Result &R, ResultW<W> &Q) {
 }
 inline void collapse4(const Result &R, Result4 &Q) { collapse<4>(R, Q); }
 
-// Quantised W-wide node (device form; Ylitie et al. 2017 style): the node's
-// box origin, one power-of-two scale per axis, the children's bounds as 8-bit
-// multiples of it rounded outward (child i in byte i % 4 of word i / 4), and
-// the links.  Child box on axis a: [origin_a + qlo * 2^e_a, origin_a + qhi *
-// 2^e_a] -- it contains the float box exactly (real arithmetic); the device's
-// slab-test rounding is of the order of ulp(D), far inside the primitives'
-// padding (rt_kernels.hip).  W = 4: 64 B (4 x 16 B), W = 8: 96 B (6 x 16 B).
+// SAH-optimal collapse (Ylitie et al. 2017, §3.1).  Over the binary tree,
+// C(n, i) is the least SAH cost of covering subtree n with at most i units,
+// each unit a leaf (<= max_leaf primitives) or a W-wide node:
+//   C(n, 1) = min(leaf: A(n) * sum(cost), node: A(n) * node_cost + dist(n, W))
+//   C(n, i) = min(C(n, i - 1), dist(n, i))
+//   dist(n, j) = min over k of C(left, k) + C(right, j - k)
+// (costs in primitive tests, A = surface area).  The binary tree should go
+// down to single primitives (Builder::max_leaf = 1): the DP picks the leaves.
 template <int W>
-struct NodeQBody {
+inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float node_cost) {
+    Q = ResultW<W>();
+    if (R.nodes.empty()) return;
+    const int ni_count = (int)R.nodes.size();
+    struct Ref {
+        int32_t link;
+        Box box;
+    };
+    auto kids = [&](int ni, Ref out[2]) {
+        const Node &n = R.nodes[ni];
+        out[0].link = n.link[0];
+        out[1].link = n.link[1];
+        for (int k = 0; k < 3; k++) out[0].box.lo[k] = n.l_lo[k];
+        out[0].box.hi[0] = n.l_hi0, out[0].box.hi[1] = n.l_hi12[0], out[0].box.hi[2] = n.l_hi12[1];
+        out[1].box.lo[0] = n.r_lo01[0], out[1].box.lo[1] = n.r_lo01[1], out[1].box.lo[2] = n.r_lo2;
+        for (int k = 0; k < 3; k++) out[1].box.hi[k] = n.r_hi[k];
+    };
+    auto leaf_sum = [&](int32_t link, int &first, int &count) {
+        int v = -link - 1;
+        first = v >> 4, count = v & 15;
+        float s = 0;
+        for (int i = first; i < first + count; i++) s += R.costs[i];
+        return s;
+    };
+    std::vector<int> first(ni_count, 0), cnt(ni_count, 0);
+    std::vector<float> psum(ni_count, 0.0f);
+    std::vector<float> C((size_t)ni_count * (W + 1), 0.0f);
+    std::vector<int8_t> D((size_t)ni_count * (W + 1), 0);   // i = 1: 0 leaf / k; i > 1: 0 "as i - 1" / k
+    auto cost = [&](const Ref &r, int i) -> float {
+        if (r.link >= 0) return C[(size_t)r.link * (W + 1) + i];
+        int f, c;
+        return r.box.area() * leaf_sum(r.link, f, c);
+    };
+    // children have larger indices than their parent (Builder::build_range)
+    for (int n = ni_count - 1; n >= 0; n--) {
+        Ref ch[2];
+        kids(n, ch);
+        Box b = ch[0].box;
+        b.grow(ch[1].box);
+        const float A = b.area();
+        int lo = INT32_MAX, num = 0;
+        float s = 0;
+        for (const Ref &r : ch) {
+            int f, c;
+            if (r.link >= 0) f = first[r.link], c = cnt[r.link], s += psum[r.link];
+            else s += leaf_sum(r.link, f, c);
+            if (c > 0) lo = std::min(lo, f);
+            num += c;
+        }
+        first[n] = num > 0 ? lo : 0, cnt[n] = num, psum[n] = s;
+        float *Cn = &C[(size_t)n * (W + 1)];
+        int8_t *Dn = &D[(size_t)n * (W + 1)];
+        auto dist = [&](int j, int &kbest) {
+            float best = INFINITY;
+            kbest = 1;
+            for (int k = 1; k < j; k++) {
+                float c = cost(ch[0], k) + cost(ch[1], j - k);
+                if (c < best) best = c, kbest = k;
+            }
+            return best;
+        };
+        int kw;
+        const float c_node = A * node_cost + dist(W, kw);
+        const float c_leaf = (num <= max_leaf && num <= 15) ? A * s : INFINITY;
+        if (c_leaf <= c_node) Cn[1] = c_leaf, Dn[1] = 0;
+        else Cn[1] = c_node, Dn[1] = (int8_t)kw;
+        for (int i = 2; i <= W; i++) {
+            int k;
+            float d = dist(i, k);
+            if (d < Cn[i - 1]) Cn[i] = d, Dn[i] = (int8_t)k;
+            else Cn[i] = Cn[i - 1], Dn[i] = 0;
+        }
+    }
+    // subtree `r` as at most i units
+    std::function<void(const Ref &, int, std::vector<Ref> &)> gather = [&](const Ref &r, int i,
+                                                                           std::vector<Ref> &out) {
+        if (r.link < 0) {
+            out.push_back(r);
+            return;
+        }
+        const int8_t *Dn = &D[(size_t)r.link * (W + 1)];
+        while (i > 1 && Dn[i] == 0) i--;
+        if (i == 1) {
+            out.push_back(r);
+            return;
+        }
+        Ref ch[2];
+        kids(r.link, ch);
+        gather(ch[0], Dn[i], out);
+        gather(ch[1], i - Dn[i], out);
+    };
+    // one unit: a leaf link or a new W-wide node (the root is always a node)
+    std::function<int32_t(const Ref &, int, int, bool)> emit = [&](const Ref &r, int depth, int stack_in,
+                                                                   bool root) -> int32_t {
+        if (r.link < 0) return r.link;
+        const int n = r.link;
+        int k = D[(size_t)n * (W + 1) + 1];
+        if (k == 0 && !root) return leaf_link(first[n], cnt[n]);
+        Ref ch2[2];
+        kids(n, ch2);
+        if (k == 0) {                                 // the root as a node although a leaf is cheaper
+            float best = INFINITY;
+            for (int j = 1; j < W; j++) {
+                float c = cost(ch2[0], j) + cost(ch2[1], W - j);
+                if (c < best) best = c, k = j;
+            }
+        }
+        std::vector<Ref> ch;
+        gather(ch2[0], k, ch);
+        gather(ch2[1], W - k, ch);
+        const int m = (int)ch.size();
+        int qi = (int)Q.nodes.size();
+        Q.nodes.emplace_back();
+        Q.depth = std::max(Q.depth, depth);
+        const int below = stack_in + (m - 1);
+        Q.max_stack = std::max(Q.max_stack, below);
+        int32_t links[W];
+        for (int i = 0; i < W; i++) links[i] = kEmpty;
+        for (int i = 0; i < m; i++) links[i] = emit(ch[i], depth + 1, below, false);
+        NodeW<W> &q = Q.nodes[qi];
+        for (int i = 0; i < W; i++) {
+            for (int a = 0; a < 3; a++) {
+                q.lo[a][i] = i < m ? ch[i].box.lo[a] : INFINITY;
+                q.hi[a][i] = i < m ? ch[i].box.hi[a] : -INFINITY;
+            }
+            q.link[i] = links[i];
+        }
+        q.max_stack = 0;
+        q.pad[0] = q.pad[1] = q.pad[2] = 0;
+        return qi;
+    };
+    Ref root;
+    root.link = 0;
+    emit(root, 1, 0, true);
+    Q.nodes[0].max_stack = Q.max_stack;
+}
+
+// Device form of a 4-wide node (80 B, 5 x 16 B; after Ylitie et al. 2017,
+// with half-precision instead of 8-bit plane offsets): the node's box origin,
+// one power-of-two scale 2^e per axis, each child's bounds as binary16
+// multiples h of it -- lower bounds rounded down, upper bounds rounded up, to
+// the binary16 grid (child i in half i % 2 of word i / 2) -- then the links.
+// Child box on axis a: [origin_a + hlo * 2^e_a, origin_a + hhi * 2^e_a]; it
+// contains the float box exactly (real arithmetic), and the device's
+// slab-test rounding is of the order of ulp(D), far inside the primitives'
+// padding (rt_kernels.hip).  The device converts h inside the plane FMA
+// (v_fma_mix_f32): no separate conversion instruction per plane, and 2^-11
+// relative resolution (8-bit offsets: 1/255) -- tighter boxes.
+struct Node4H {
     float origin[3];
     int8_t exp[4];           // exponents e of the x, y, z scales 2^e (-126 <= e <= kQExpMax); [3] unused
-    uint32_t qlo[3][W / 4];  // per axis: lower bounds
-    uint32_t qhi[3][W / 4];  // per axis: upper bounds
-    int32_t link[W];
+    uint32_t lo[3][2];       // per axis: lower bounds of children (0, 1), (2, 3)
+    uint32_t hi[3][2];       // per axis: upper bounds
+    int32_t link[4];
 };
-template <int W>
-struct NodeQ : NodeQBody<W> {
-    int32_t pad[2];
-};
-template <>
-struct NodeQ<8> : NodeQBody<8> {};
-using Node4Q = NodeQ<4>;
-using Node8Q = NodeQ<8>;
-static_assert(sizeof(Node4Q) == 64, "quantised node4 layout");
-static_assert(sizeof(Node8Q) == 96, "quantised node8 layout");
+static_assert(sizeof(Node4H) == 80, "node4 device layout");
 
+// h in [0, kHMax]: 2048 keeps the offsets where binary16 is integer-exact
+constexpr double kHMax = 2048.0;
 // Largest scale exponent: the device forms 2^e * (1/d) with |1/d| capped at
-// 2^100, which stays finite for e <= 27 (node extents up to 255 * 2^27).
+// 2^100, which stays finite for e <= 27 (node extents up to 2048 * 2^27).
 constexpr int kQExpMax = 27;
+// empty slot: an inverted box in every axis (lower bound kHMax, upper 0)
+constexpr uint16_t kHalfHMax = 0x6800;   // 2048.0 in binary16
+
+// bits of a non-negative double that is a binary16 value
+inline uint16_t half_bits(double r) {
+    if (!(r > 0)) return 0;
+    int k;
+    std::frexp(r, &k);                       // r in [2^(k-1), 2^k)
+    const int E = k - 1;
+    if (E < -14) return (uint16_t)std::ldexp(r, 24);                       // subnormal
+    return (uint16_t)(((E + 15) << 10) | ((uint32_t)std::ldexp(r, 10 - E) - 1024u));
+}
+// the largest binary16 value <= v (up = false) or the smallest >= v (up =
+// true), for v in [0, kHMax]
+inline uint16_t half_round(double v, bool up) {
+    if (!(v > 0)) return 0;
+    int k;
+    std::frexp(v, &k);
+    const double ulp = std::ldexp(1.0, std::max(k - 1, -14) - 10);
+    const double m = up ? std::ceil(v / ulp) : std::floor(v / ulp);
+    return half_bits(m * ulp);               // exact: m < 2^12, ulp a power of two
+}
+// value of binary16 bits (non-negative)
+inline double half_value(uint16_t b) {
+    const int E = (b >> 10) & 31, m = b & 1023;
+    return E == 0 ? std::ldexp((double)m, -24) : std::ldexp(1024.0 + m, E - 25);
+}
 
 // Returns false if a child box is not finite (NaN/inf geometry) or a node is
 // too large for kQExpMax: the caller then uses the brute-force scan.
-template <int W>
-inline bool quantize(const ResultW<W> &Q, std::vector<NodeQ<W>> &out) {
-    out.assign(Q.nodes.size(), NodeQ<W>{});
+inline bool quantize(const Result4 &Q, std::vector<Node4H> &out) {
+    out.assign(Q.nodes.size(), Node4H{});
     for (size_t k = 0; k < Q.nodes.size(); k++) {
-        const NodeW<W> &n = Q.nodes[k];
-        NodeQ<W> &z = out[k];
-        for (int i = 0; i < W; i++) z.link[i] = n.link[i];
+        const Node4 &n = Q.nodes[k];
+        Node4H &z = out[k];
+        for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
         z.exp[3] = 0;
         for (int a = 0; a < 3; a++) {
             auto empty = [&](int i) {              // no slot, or an empty leaf (inverted box)
                 return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]);
             };
             double lo = INFINITY, hi = -INFINITY;
-            for (int i = 0; i < W; i++) {
+            for (int i = 0; i < 4; i++) {
                 if (empty(i)) continue;
                 if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
                 lo = std::min(lo, (double)n.lo[a][i]);
@@ -211,31 +380,28 @@ inline bool quantize(const ResultW<W> &Q, std::vector<NodeQ<W>> &out) {
             }
             if (!(lo <= hi)) lo = hi = 0.0;              // no child at all
             z.origin[a] = (float)lo;                     // exact: lo is a float
-            // smallest scale 2^e with 255 * 2^e >= extent (normal floats only)
+            // smallest scale 2^e with kHMax * 2^e >= extent (normal floats only)
             double ext = hi - lo;
             int e = -126;
-            while (e < 127 && std::ldexp(255.0, e) < ext) e++;
+            while (e < 127 && std::ldexp(kHMax, e) < ext) e++;
             if (e > kQExpMax) return false;
             z.exp[a] = (int8_t)e;
             double sc = std::ldexp(1.0, e);
-            for (int w = 0; w < W / 4; w++) z.qlo[a][w] = z.qhi[a][w] = 0;
-            for (int i = 0; i < W; i++) {
-                uint32_t l = 255, h = 0;                 // empty slot: inverted box
+            z.lo[a][0] = z.lo[a][1] = z.hi[a][0] = z.hi[a][1] = 0;
+            for (int i = 0; i < 4; i++) {
+                uint32_t l = kHalfHMax, h = 0;           // empty slot: inverted box
                 if (!empty(i)) {
                     // exact in double: float differences, power-of-two scale
-                    double fl = std::floor(((double)n.lo[a][i] - lo) / sc);
-                    double fh = std::ceil(((double)n.hi[a][i] - lo) / sc);
-                    l = (uint32_t)std::max(0.0, std::min(255.0, fl));
-                    h = (uint32_t)std::max(0.0, std::min(255.0, fh));
+                    l = half_round(std::min(kHMax, ((double)n.lo[a][i] - lo) / sc), false);
+                    h = half_round(std::min(kHMax, ((double)n.hi[a][i] - lo) / sc), true);
                 }
-                z.qlo[a][i / 4] |= l << (8 * (i % 4));
-                z.qhi[a][i / 4] |= h << (8 * (i % 4));
+                z.lo[a][i / 2] |= l << (16 * (i % 2));
+                z.hi[a][i / 2] |= h << (16 * (i % 2));
             }
         }
     }
     return true;
 }
-inline bool quantize4(const Result4 &Q, std::vector<Node4Q> &out) { return quantize<4>(Q, out); }
 
 // Renumber Q's nodes breadth-first (root stays 0), so that the top levels of
 // the tree are nodes [0, K) for any K.
@@ -334,7 +500,8 @@ class Builder {
         set_child(R.nodes[0], 1, bounds(mid, (int)P.size()), r);
         R.depth = std::max(R.depth, 1);
         R.keys.resize(P.size());
-        for (size_t i = 0; i < P.size(); i++) R.keys[i] = P[idx[i]].key;
+        R.costs.resize(P.size());
+        for (size_t i = 0; i < P.size(); i++) R.keys[i] = P[idx[i]].key, R.costs[i] = P[idx[i]].cost;
         return R.depth <= kMaxDepth;
     }
 

@@ -345,7 +345,9 @@ __device__ __forceinline__ float own_nearest(const Query &q, const Params &p, in
 }
 
 
-constexpr int kNodeF4 = 4;                       // float4 per quantised 4-wide node (rt_bvh.h Node4Q)
+constexpr int kNodeF4 = 5;                       // float4 per 4-wide node (rt_bvh.h Node4H)
+static_assert(kNodeF4 * 16 == sizeof(rtbvh::Node4H), "node layout");
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plane offsets
 // while-while traversal: stop descending when at most this many lanes still
 // look for a leaf (A/B, C3 Mrays/s: 0 -> 5912, 1 -> 5960, 2 -> 5957, 3 -> 5954,
 // 6 -> 5924, 12 -> 5849; with one leaf per round: 0 -> 5885, 2 -> 6021,
@@ -491,12 +493,13 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
         }
         return n;
     };
-    // One quantised 4-wide node (rt_bvh.h Node4Q): plane a of child i at
-    // origin_a + q * 2^e_a, i.e. t = q * (2^e_a / d_a) + (origin_a - o_a) / d_a
-    // = fma(q, A_a, B_a) -- one fma per plane; the rounding (~ulp(D) in
-    // distance) is far inside the primitive padding.  Slab-test the children,
-    // push the far hits, continue with the nearest, park the first leaf reached.
-    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3) {
+    // One 4-wide node (rt_bvh.h Node4H): plane a of child i at origin_a +
+    // h * 2^e_a (h binary16), i.e. t = h * (2^e_a / d_a) + (origin_a - o_a) / d_a
+    // = fma(h, A_a, B_a) -- one v_fma_mix_f32 per plane (h converted inside
+    // the fma, exactly); the rounding (~ulp(D) in distance) is far inside the
+    // primitive padding.  Slab-test the children, push the far hits, continue
+    // with the nearest, park the first leaf reached.
+    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3, float4 w4) {
 #if RT_PROF
         cnt.trips++;
 #endif
@@ -509,22 +512,31 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
         float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
         float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
         float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
-        unsigned qlx = __float_as_uint(w1.x), qly = __float_as_uint(w1.y), qlz = __float_as_uint(w1.z);
-        unsigned qhx = __float_as_uint(w1.w), qhy = __float_as_uint(w2.x), qhz = __float_as_uint(w2.y);
-        int c0 = __float_as_int(w2.z), c1 = __float_as_int(w2.w), c2 = __float_as_int(w3.x), c3 = __float_as_int(w3.y);
-        // near / far plane per axis by the ray's octant: t(q) = fma(q, A, B) is
-        // monotonic in q with the sign of A (= the sign of 1/d), so
+        // lower / upper bounds per axis, two children per word
+        const unsigned lx[2] = {__float_as_uint(w1.x), __float_as_uint(w1.y)};
+        const unsigned ly[2] = {__float_as_uint(w1.z), __float_as_uint(w1.w)};
+        const unsigned lz[2] = {__float_as_uint(w2.x), __float_as_uint(w2.y)};
+        const unsigned hx[2] = {__float_as_uint(w2.z), __float_as_uint(w2.w)};
+        const unsigned hy[2] = {__float_as_uint(w3.x), __float_as_uint(w3.y)};
+        const unsigned hz[2] = {__float_as_uint(w3.z), __float_as_uint(w3.w)};
+        int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
+        // near / far plane per axis by the ray's octant: t(h) = fma(h, A, B) is
+        // monotonic in h with the sign of A (= the sign of 1/d), so
         // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10
-        const unsigned nx = neg_x ? qhx : qlx, fx = neg_x ? qlx : qhx;
-        const unsigned ny = neg_y ? qhy : qly, fy = neg_y ? qly : qhy;
-        const unsigned nz = neg_z ? qhz : qlz, fz = neg_z ? qlz : qhz;
+        h2v nx[2], fx[2], ny[2], fy[2], nz[2], fz[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            nx[j] = __builtin_bit_cast(h2v, neg_x ? hx[j] : lx[j]), fx[j] = __builtin_bit_cast(h2v, neg_x ? lx[j] : hx[j]);
+            ny[j] = __builtin_bit_cast(h2v, neg_y ? hy[j] : ly[j]), fy[j] = __builtin_bit_cast(h2v, neg_y ? ly[j] : hy[j]);
+            nz[j] = __builtin_bit_cast(h2v, neg_z ? hz[j] : lz[j]), fz[j] = __builtin_bit_cast(h2v, neg_z ? lz[j] : hz[j]);
+        }
         float k[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int sh = 8 * i;
-            float tnx = fmaf((float)((nx >> sh) & 0xffu), Ax, Bx), tfx = fmaf((float)((fx >> sh) & 0xffu), Ax, Bx);
-            float tny = fmaf((float)((ny >> sh) & 0xffu), Ay, By), tfy = fmaf((float)((fy >> sh) & 0xffu), Ay, By);
-            float tnz = fmaf((float)((nz >> sh) & 0xffu), Az, Bz), tfz = fmaf((float)((fz >> sh) & 0xffu), Az, Bz);
+            const int j = i / 2, e = i % 2;
+            float tnx = fmaf((float)nx[j][e], Ax, Bx), tfx = fmaf((float)fx[j][e], Ax, Bx);
+            float tny = fmaf((float)ny[j][e], Ay, By), tfy = fmaf((float)fy[j][e], Ay, By);
+            float tnz = fmaf((float)nz[j][e], Az, Bz), tfz = fmaf((float)fz[j][e], Az, Bz);
             if (!point) {
                 float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
                 float tf = fminf(fminf(tfx, tfy), fminf(tfz, thi));
@@ -591,19 +603,19 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
     if (point)
         node = root;
     else
-        visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3));
+        visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4));
     for (;;) {
         while (node >= 0) {
 #if RT_PROF >= 2
             const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
             const float4 *N = p.bvh + kNodeF4 * node;
-            float4 w0 = N[0], w1 = N[1], w2 = N[2], w3 = N[3];
+            float4 w0 = N[0], w1 = N[1], w2 = N[2], w3 = N[3], w4 = N[4];
 #if RT_PROF >= 2
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w3.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
-            visit_q(w0, w1, w2, w3);
+            visit_q(w0, w1, w2, w3, w4);
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
@@ -1504,6 +1516,9 @@ struct rt_scene {
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
     long long opt_bvh_leaf = 8;        // SAH max leaf size
     long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
+    long long opt_bvh_collapse = 1;    // binary -> 4-wide: 0 greedy (largest area first), 1 SAH-optimal DP
+    long long opt_bvh_node = 500;      // DP collapse: cost of a 4-wide node visit, x1000 of a sphere test
+                                       // (A/B, C3: 0.25 / 0.5 / 0.75 / 1 / 2 -> +0.6 / +0.5 / +0.5 / +0.2 / -1.7 %)
     long long opt_fail_bvh_upload = 0; // test hook: the next BVH uploads fail (RT_E_NOMEM)
     // BVH inputs kept on the host (the boxes' padding depends on the eye)
     struct PrimSrc {
@@ -1616,6 +1631,22 @@ double distance_bound(const rt_scene *s, const float eye[3]) {
     return std::max(std::sqrt(diag2), std::sqrt(far2)) + mag + 1.0;
 }
 
+// Binary SAH tree over P, collapsed into 4-wide nodes (opt_bvh_collapse: 0
+// greedy, largest child area first; 1 SAH-optimal) and renumbered breadth-first
+// (the top levels first: cache locality of the hot nodes).
+bool build_wide(rt_scene *s, std::vector<rtbvh::Prim> &P, rtbvh::Result &R, rtbvh::Result4 &Q) {
+    rtbvh::Builder B(P);
+    B.max_leaf = s->opt_bvh_collapse ? 1 : (int)s->opt_bvh_leaf;
+    B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
+    if (!B.build(R) || R.nodes.empty()) return false;
+    if (s->opt_bvh_collapse)
+        rtbvh::collapse_sah<4>(R, Q, (int)s->opt_bvh_leaf, (float)s->opt_bvh_node / 1000.0f);
+    else
+        rtbvh::collapse<4>(R, Q);
+    rtbvh::bfs_order(Q);
+    return true;
+}
+
 // Shadow-cone tree of a directional light (Params::dirk, dir_bf == 2).
 //
 // The reference's directional shadow ray runs TraceRay with the light's
@@ -1641,7 +1672,7 @@ double distance_bound(const rt_scene *s, const float eye[3]) {
 // k is rounded up.  Returns false if the direction or the geometry is not
 // finite, or the scene is so large that one ulp of B reaches epsilon (then
 // the h < 0 side is no longer safe): the caller falls back to the scan.
-bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4Q> &nodes, std::vector<float4> &rec,
+bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4H> &nodes, std::vector<float4> &rec,
               DirK &out) {
     for (int k = 0; k < 9; k++) out.R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
     out.root = -1;
@@ -1697,14 +1728,8 @@ bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4Q
     out.cone_k = std::nextafter((float)(std::max(0.0, s2 - 1.0) * (1.0 + std::ldexp(1.0, -16))), INFINITY);
     if (s2 < 1.0) out.cone_h = std::nextafter((float)(re_max / std::sqrt(1.0 - s2) + pad), INFINITY);
     rtbvh::Result Rb;
-    rtbvh::Builder B(P);
-    B.max_leaf = (int)s->opt_bvh_leaf;
-    B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
-    if (!B.build(Rb) || Rb.nodes.empty()) return false;
     rtbvh::Result4 Q;
-    rtbvh::collapse<4>(Rb, Q);
-    rtbvh::bfs_order(Q);
-    if (Q.max_stack > kStack) return false;
+    if (!build_wide(s, P, Rb, Q) || Q.max_stack > kStack) return false;
     const int nf = s->base.nf;
     bool ok = rtbvh::leaf_records(
         Q, Rb.keys, [](int32_t) { return false; },
@@ -1716,7 +1741,7 @@ bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4Q
             return 2;
         },
         rec.size());
-    std::vector<rtbvh::Node4Q> QQ;
+    std::vector<rtbvh::Node4H> QQ;
     if (!ok || !rtbvh::quantize(Q, QQ)) return false;
     const int base = (int)nodes.size();
     for (auto &z : QQ) {
@@ -1769,15 +1794,8 @@ int build_bvh(rt_scene *s, double D) {
         }
     }
     rtbvh::Result R;
-    rtbvh::Builder B(P);
-    B.max_leaf = (int)s->opt_bvh_leaf;
-    B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
-    bool ok = B.build(R);
     rtbvh::Result4 Q;
-    if (ok && !R.nodes.empty()) {
-        rtbvh::collapse<4>(R, Q);
-        rtbvh::bfs_order(Q);                 // top levels first (cache locality of the hot nodes)
-    }
+    bool ok = P.empty() || build_wide(s, P, R, Q);
     // leaf records: face = its 5 scan words with (key, shadow factor) in the
     // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
     std::vector<float4> rec;
@@ -1798,7 +1816,7 @@ int build_bvh(rt_scene *s, double D) {
             return 2;
         });
     rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
-    std::vector<rtbvh::Node4Q> QQ;
+    std::vector<rtbvh::Node4H> QQ;
     if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ)) ok = false;     // non-finite geometry: scan
     for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
         for (auto &l : z.link)
@@ -2170,9 +2188,11 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         if (value < 12 || value > kLdsStack) return RT_E_INVALID;
         s->base.stack_cap = (int)value;
     }
-    else if (k == "bvh_leaf" || k == "bvh_trav") {
+    else if (k == "bvh_leaf" || k == "bvh_trav" || k == "bvh_collapse" || k == "bvh_node") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
-        else s->opt_bvh_trav = std::max(0LL, value);
+        else if (k == "bvh_trav") s->opt_bvh_trav = std::max(0LL, value);
+        else if (k == "bvh_collapse") s->opt_bvh_collapse = value != 0;
+        else s->opt_bvh_node = std::max(0LL, value);
         s->bvh_D = -1.0;               // rebuild on the next render
     }
     else return RT_E_INVALID;

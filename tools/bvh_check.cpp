@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -18,12 +19,57 @@ static bool contains(const float lo[3], const float hi[3], const Box &b) {
     return true;
 }
 
+// SAH cost of a wide tree (collapse_sah's model): node boxes x node_cost,
+// leaf boxes x the sum of their primitives' costs
 template <int W>
-static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int &nodes, int &depth, int &stack) {
+static double sah_cost(const ResultW<W> &Q, const Result &R, float node_cost) {
+    double c = 0;
+    for (const NodeW<W> &nd : Q.nodes) {
+        Box nb;
+        for (int i = 0; i < W; i++) {
+            if (nd.link[i] == kEmpty) continue;
+            Box b;
+            for (int k = 0; k < 3; k++) b.lo[k] = nd.lo[k][i], b.hi[k] = nd.hi[k][i];
+            nb.grow(b);
+            if (nd.link[i] < 0) {
+                int v = -nd.link[i] - 1, first = v >> 4, count = v & 15;
+                double s = 0;
+                for (int q = first; q < first + count; q++) s += R.costs[q];
+                c += b.area() * s;
+            }
+        }
+        c += nb.area() * node_cost;
+    }
+    return c;
+}
+
+// mode 0: greedy collapse; 1: SAH-optimal collapse (R built down to single
+// primitives), whose SAH cost must not exceed the greedy collapse's of R
+template <int W>
+static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int &nodes, int &depth, int &stack,
+                      int mode = 0) {
     const float inf = INFINITY;
     // 4-wide collapse: same leaves, contained boxes, every slot valid or empty
     ResultW<W> Q;
-    collapse<W>(R, Q);
+    if (mode == 1) {
+        collapse_sah<W>(R, Q, 8, 1.0f);
+        ResultW<W> G;
+        collapse<W>(R, G);
+        double cs = sah_cost(Q, R, 1.0f), cg = sah_cost(G, R, 1.0f);
+        if (!(cs <= cg * (1 + 1e-5))) { printf("FAIL sah collapse cost %g > greedy %g\n", cs, cg); return 1; }
+        // leaves above max_leaf only where the binary tree has them (coincident centroids)
+        std::vector<int32_t> bin;
+        for (const Node &b : R.nodes) bin.push_back(b.link[0]), bin.push_back(b.link[1]);
+        for (const NodeW<W> &nd : Q.nodes)
+            for (int i = 0; i < W; i++)
+                if (nd.link[i] < 0 && nd.link[i] != kEmpty && ((-nd.link[i] - 1) & 15) > 8 &&
+                    std::find(bin.begin(), bin.end(), nd.link[i]) == bin.end()) {
+                    printf("FAIL sah leaf size\n");
+                    return 1;
+                }
+    } else {
+        collapse<W>(R, Q);
+    }
     size_t n4 = Q.nodes.size();
     bfs_order(Q);
     {   // breadth-first: same node count, depth non-decreasing with the index
@@ -74,21 +120,35 @@ static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int
     }
     if (cov4 != n) { printf("FAIL covered4 %d of %d\n", cov4, n); return 1; }
     if (maxstack > Q.max_stack || Q.nodes[0].max_stack != Q.max_stack) { printf("FAIL max_stack\n"); return 1; }
-    // quantised nodes contain the float child boxes exactly (real arithmetic)
-    {
-        std::vector<NodeQ<W>> QQ;
-        if (!quantize<W>(Q, QQ)) { printf("FAIL quantize4\n"); return 1; }
+    // device nodes (binary16 offsets) contain the float child boxes exactly (real arithmetic)
+    if (W == 4) {
+        std::vector<Node4H> QQ;
+        ResultW<4> Q4;
+        Q4.nodes.resize(Q.nodes.size());
+        for (size_t k = 0; k < Q.nodes.size(); k++) {
+            for (int a = 0; a < 3; a++)
+                for (int i = 0; i < 4; i++) Q4.nodes[k].lo[a][i] = Q.nodes[k].lo[a][i], Q4.nodes[k].hi[a][i] = Q.nodes[k].hi[a][i];
+            for (int i = 0; i < 4; i++) Q4.nodes[k].link[i] = Q.nodes[k].link[i];
+        }
+        if (!quantize(Q4, QQ)) { printf("FAIL quantize4\n"); return 1; }
         for (size_t k = 0; k < Q.nodes.size(); k++)
             for (int a = 0; a < 3; a++) {
                 double sc = std::ldexp(1.0, (int)QQ[k].exp[a]), o = QQ[k].origin[a];
-                for (int i = 0; i < W; i++) {
-                    unsigned l = (QQ[k].qlo[a][i / 4] >> (8 * (i % 4))) & 255, h = (QQ[k].qhi[a][i / 4] >> (8 * (i % 4))) & 255;
-                    if (Q.nodes[k].link[i] == kEmpty || !(Q.nodes[k].lo[a][i] <= Q.nodes[k].hi[a][i])) {
+                for (int i = 0; i < 4; i++) {
+                    double l = half_value((QQ[k].lo[a][i / 2] >> (16 * (i % 2))) & 0xffff);
+                    double h = half_value((QQ[k].hi[a][i / 2] >> (16 * (i % 2))) & 0xffff);
+                    if (Q4.nodes[k].link[i] == kEmpty || !(Q4.nodes[k].lo[a][i] <= Q4.nodes[k].hi[a][i])) {
                         if (!(l > h)) { printf("FAIL quantize4 empty slot\n"); return 1; }
                         continue;
                     }
-                    if (!(o + l * sc <= Q.nodes[k].lo[a][i]) || !(o + h * sc >= Q.nodes[k].hi[a][i])) {
+                    if (!(o + l * sc <= Q4.nodes[k].lo[a][i]) || !(o + h * sc >= Q4.nodes[k].hi[a][i])) {
                         printf("FAIL quantize4 containment\n");
+                        return 1;
+                    }
+                    // tight: one binary16 step of slack at most
+                    if ((Q4.nodes[k].lo[a][i] - (o + l * sc)) > sc * std::max(1.0, l) * 0x1p-10 + 1e-30 ||
+                        ((o + h * sc) - Q4.nodes[k].hi[a][i]) > sc * std::max(1.0, h) * 0x1p-10 + 1e-30) {
+                        printf("FAIL quantize4 loose\n");
                         return 1;
                     }
                 }
@@ -139,6 +199,19 @@ static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int
 }
 
 int main(int argc, char **argv) {
+    // binary16 helpers: every non-negative finite value round-trips, and the
+    // directed roundings bracket a value by neighbouring grid points
+    for (uint32_t b = 0; b < 0x7c00; b++) {
+        double v = half_value((uint16_t)b);
+        if (half_bits(v) != b || half_round(v, false) != b || half_round(v, true) != b) {
+            printf("FAIL half bits %u\n", b);
+            return 1;
+        }
+        if (b + 1 < 0x7c00 && v < kHMax) {
+            double m = 0.5 * (v + half_value((uint16_t)(b + 1)));
+            if (half_round(m, false) != b || half_round(m, true) != b + 1) { printf("FAIL half round %u\n", b); return 1; }
+        }
+    }
     int n = argc > 1 ? atoi(argv[1]) : 1000;
     int seed = argc > 2 ? atoi(argv[2]) : 1;
     int mode = argc > 3 ? atoi(argv[3]) : 0;   // 0 random, 1 all coincident, 2 a line
@@ -198,10 +271,19 @@ int main(int argc, char **argv) {
     }
     if (covered != n) { printf("FAIL covered %d of %d\n", covered, n); return 1; }
     (void)r;
-    int n4, d4, s4, n8, d8, s8;
+    int n4, d4, s4, n8, d8, s8, nq, dq, sq;
     if (check_wide<4>(R, orig, n, n4, d4, s4)) return 1;
     if (check_wide<8>(R, orig, n, n8, d8, s8)) return 1;
+    {   // SAH-optimal collapse of a tree built down to single primitives
+        std::vector<Prim> P1 = orig;
+        Result R1;
+        Builder B1(P1);
+        B1.max_leaf = 1;
+        if (!B1.build(R1)) { printf("FAIL depth (max_leaf 1) %d\n", R1.depth); return 1; }
+        if (check_wide<4>(R1, orig, n, nq, dq, sq, 1)) return 1;
+    }
     printf("OK n=%d nodes=%zu leaves=%d depth=%d walk_depth=%d nodes4=%d depth4=%d stack4=%d nodes8=%d depth8=%d "
-           "stack8=%d\n", n, R.nodes.size(), leaves, R.depth, maxd, n4, d4, s4, n8, d8, s8);
+           "stack8=%d sah4: nodes=%d depth=%d stack=%d\n", n, R.nodes.size(), leaves, R.depth, maxd, n4, d4, s4, n8,
+           d8, s8, nq, dq, sq);
     return 0;
 }
