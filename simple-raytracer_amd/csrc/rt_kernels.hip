@@ -374,10 +374,13 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
         int nt = 0;
         int key;
         float fac;
-        // one batch of loads for either kind (a sphere reads 3 words past its
-        // record; the stream is padded for the last one)
+        // one batch of loads for either kind; the face words 2..4 only when
+        // some lane of the wave is at a face (a sphere then reads 3 words past
+        // its record; the stream is padded for the last one) -- the vector
+        // memory path (TA), not the ALU, is the busier one here
         const f4v *RV = reinterpret_cast<const f4v *>(R);
-        f4v w0 = RV[0], w1 = RV[1], w2 = RV[2], w3 = RV[3], w4 = RV[4];
+        f4v w0 = RV[0], w1 = RV[1], w2 = {0.0f, 0.0f, 0.0f, 0.0f}, w3 = w2, w4 = w2;
+        if (__ballot(k < nfc)) w2 = RV[2], w3 = RV[3], w4 = RV[4];
         asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
         float4 f0 = make_float4(w0.x, w0.y, w0.z, w0.w), f1 = make_float4(w1.x, w1.y, w1.z, w1.w);
         float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
