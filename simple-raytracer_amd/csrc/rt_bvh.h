@@ -479,7 +479,7 @@ class Builder {
     int max_leaf = 8;                       // SAH leaves (<= 15 fits the link encoding)
     float trav_cost = 1.0f;                 // SAH cost of one node visit, in sphere tests
     static constexpr int kSahDepth = 22;    // deeper: object-median splits (bounded depth)
-    static constexpr int kMaxDepth = 40;    // the device traversal stack holds 40 entries
+    static constexpr int kMaxDepth = 64;    // binary depth cap (object-median splits below kSahDepth keep it low)
 
     explicit Builder(std::vector<Prim> &prims) : P(prims) {}
 

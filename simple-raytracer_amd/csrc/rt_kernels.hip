@@ -160,10 +160,10 @@ struct Params {
                                          // 1 brute-force scan, 2 faces by the BVH + shadow-region trees
     const DirK *__restrict__ dirk;       // per light (dir_bf == 2)
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
-    int bvh_stack;                       // BVH: worst-case traversal stack entries of the tree
+    int ovf_stride;                      // BVH: stack spill entries per lane (deepest tree, kSpill multiple)
     int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
     void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
-    int *__restrict__ ovf;               // grid x kBlock x kStack spilled BVH stack entries
+    int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -173,14 +173,17 @@ enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif
-constexpr int kStack = 40;               // max per-lane BVH stack entries (deeper trees: the scan)
+// Largest worst-case BVH stack a tree may need (entries per lane; the spill
+// area is sized per tree, Params::ovf_stride).  Refill tags kRefill + b stay
+// far below the leaf links (> INT_MIN + 256) for b <= kStackMax / kSpill.
+constexpr int kStackMax = 1024;
 // BVH traversal stack entries per lane in LDS (entry 0: the sentinel); a
 // deeper stack spills its oldest kSpill entries to device memory (rare)
 constexpr int kLdsStack = 16;            // most entries the LDS share may hold (option lds_stack)
 constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading state): 5 blocks per CU
                                          // on paper, -8.6 % measured; 14: 270 spills per C3 frame
 constexpr int kSpill = 8;
-static_assert(kStack % kSpill == 0 && kLdsStack - 3 > kSpill, "stack spill blocks");
+static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack - 3 > kSpill, "stack spill blocks");
 constexpr int kBlock = 256;
 
 // ---------------------------------------------------------------------------
@@ -472,7 +475,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
     // LDS holds stack entries [0, kLdsStack); entry 0 is kEmpty, or kRefill + b
     // when b blocks of kSpill older entries wait in device memory (ovf).
     auto ovf_lane = [&]() -> int * {
-        return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * kStack;
+        return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * p.ovf_stride;
     };
     auto spill = [&]() {                       // move the oldest kSpill entries out
         const int tag = stk[0];
@@ -486,7 +489,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
     };
     auto pop = [&]() -> int {
         int n = stk[(--sp) * kBlock];
-        if ((unsigned)n - (unsigned)kRefill - 1u < (unsigned)(kStack / kSpill)) {   // rare: bring a block back
+        if ((unsigned)n - (unsigned)kRefill - 1u < (unsigned)(kStackMax / kSpill)) {   // rare: bring a block back
             const int nb = n - kRefill;
             const int *o = ovf_lane() + (nb - 1) * kSpill;
             for (int i = 0; i < kSpill; i++) stk[(1 + i) * kBlock] = o[i];
@@ -1543,6 +1546,7 @@ struct rt_scene {
 
     int bvh_depth = 0;
     int bvh_stack = 0;
+    int ovf_stride = kSpill;           // spilled BVH stack entries per lane (Params::ovf_stride)
     bool bvh_ok = false;
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
@@ -1588,7 +1592,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     if (grid < 1) grid = 1;
     Params pl = p;
     const size_t cold_bytes = (size_t)grid * kBlock * MAXF * sizeof(Cold<MAXF>);
-    size_t fbytes = cold_bytes + (size_t)grid * kBlock * kStack * sizeof(int);
+    size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
@@ -1676,7 +1680,7 @@ bool build_wide(rt_scene *s, std::vector<rtbvh::Prim> &P, rtbvh::Result &R, rtbv
 // finite, or the scene is so large that one ulp of B reaches epsilon (then
 // the h < 0 side is no longer safe): the caller falls back to the scan.
 bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4H> &nodes, std::vector<float4> &rec,
-              DirK &out) {
+              DirK &out, int &max_stack) {
     for (int k = 0; k < 9; k++) out.R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
     out.root = -1;
     out.cone_k = 0.0f;
@@ -1732,7 +1736,8 @@ bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4H
     if (s2 < 1.0) out.cone_h = std::nextafter((float)(re_max / std::sqrt(1.0 - s2) + pad), INFINITY);
     rtbvh::Result Rb;
     rtbvh::Result4 Q;
-    if (!build_wide(s, P, Rb, Q) || Q.max_stack > kStack) return false;
+    if (!build_wide(s, P, Rb, Q) || Q.max_stack > kStackMax) return false;
+    max_stack = Q.max_stack;
     const int nf = s->base.nf;
     bool ok = rtbvh::leaf_records(
         Q, Rb.keys, [](int32_t) { return false; },
@@ -1824,18 +1829,22 @@ int build_bvh(rt_scene *s, double D) {
     for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
         for (auto &l : z.link)
             if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
-    // the device stack holds kStack entries: a deeper tree uses the scan
-    ok = ok && !Q.nodes.empty() && Q.max_stack <= kStack;
+    // the spill area is sized for the deepest tree (kStackMax: far beyond any
+    // tree the builder's depth cap allows)
+    ok = ok && !Q.nodes.empty() && Q.max_stack <= kStackMax;
     // directional lights in a scene with spheres: shadow-region trees, after
     // the main tree in the same node and record arrays
     std::vector<DirK> dirk(s->h_lights.size());
     int dir_mode = 0;
+    int stack_all = Q.max_stack;                 // deepest stack over the main and the cone trees
     if (ok && s->base.ns > 0) {
         rec.resize(rec.size() - 3);                  // the 3 padding words go after the last tree
         for (size_t l = 0; l < s->h_lights.size(); l++) {
             if (s->h_lights[l].w != 0.0f) continue;
             if (dir_mode == 0) dir_mode = 2;
-            if (!dir_tree(s, s->h_lights[l], D, QQ, rec, dirk[l])) dir_mode = 1;
+            int st = 0;
+            if (!dir_tree(s, s->h_lights[l], D, QQ, rec, dirk[l], st)) dir_mode = 1;
+            stack_all = std::max(stack_all, st);
         }
         rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
         if ((rec.size() >> 8) >= (1u << 23) - 2) ok = false;
@@ -1888,6 +1897,8 @@ int build_bvh(rt_scene *s, double D) {
     s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
     s->bvh_depth = s->bvh_ok ? Q.depth : 0;
     s->bvh_stack = s->bvh_ok ? Q.max_stack : 0;
+    // spill area per lane: every block of kSpill entries a stack can push out
+    s->ovf_stride = s->bvh_ok ? (stack_all / kSpill + 1) * kSpill : kSpill;
     s->bvh_nodes = s->bvh_ok ? (long long)Q.nodes.size() : 0;
     s->bvh_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return rc;
@@ -1911,7 +1922,7 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
             p.leafrec = s->base.leafrec;
             p.dirk = s->base.dirk;
             p.dir_bf = s->base.dir_bf;
-            p.bvh_stack = std::max(1, s->bvh_stack);
+            p.ovf_stride = s->ovf_stride;
         }
     }
     if (mode == MODE_SCAN) {

@@ -431,6 +431,42 @@ def test_degenerate_scenes(body, kind, accel, tmp_path):
         assert cnt["shadow"] == cnt["reflection"] == cnt["refraction"] == 0
 
 
+def _deep_scene_text(w: int = 32, h: int = 32) -> str:
+    """Four arms of spheres at geometrically growing distance (1.08^k, k < 200)
+    from the view axis and along it: a skewed tree (worst-case stack 27 with
+    the device's padding; tools/bvh_check mode 4 estimates it on the host)."""
+    import math
+    out = [gen.HEADER.format(w=w, h=h), "light -10 10 0 1 0.6 0.6 0.6\n", "light 10 8 -10 1 0.6 0.6 0.6\n"]
+    for i in range(800):
+        k, arm = i % 200, i // 200
+        d, ang = 1.08 ** k, arm * math.pi / 2
+        glass = " 0.3 1.5" if i % 10 == 0 else ""
+        out.append(f"mtlcolor 0.{i % 7 + 2} 0.5 0.{i % 5 + 3} 1 1 1 0.2 0.6 0.5 20{glass}\n")
+        out.append(f"sphere {math.cos(ang) * d * 0.3:.6f} {math.sin(ang) * d * 0.3:.6f} {-(5 + d):.6f} 0.4\n")
+    return "".join(out)
+
+
+def test_deep_stack_tree(tmp_path):
+    """The stack spill area is sized per tree (Params::ovf_stride, from the
+    deepest of the main and cone trees).  A skewed tree whose worst-case stack
+    is about twice the 12-entry LDS share spills two blocks deep and brings
+    them back; the image and ray counts match the oracle."""
+    (tmp_path / "deep.txt").write_text(_deep_scene_text())
+    for opts in ({}, {"lds_stack": 12}):
+        hs = rtamd.HostScene("deep.txt", cwd=str(tmp_path))
+        W, H = hs.width, hs.height
+        gs = rtamd.GpuScene(hs)
+        for k, v in opts.items():
+            gs.set_option(k, v)
+        img, st = gs.render_rows(hs.camera(), W, H, 0, H)
+        dbg = gs.debug_counters()
+        assert dbg[16] == 2 and dbg[22] >= 24, (dbg[16], dbg[22])      # BVH mode, a deep worst case
+        ref, cnt = OracleScene("deep.txt", cwd=str(tmp_path)).render()
+        assert_parity(img, ref, f"deep stack {opts}")
+        assert _counts(st) == cnt
+        _summary[f"deep_stack_{opts}"] = dict(stack=dbg[22], spills=st.stack_spills)
+
+
 def test_lds_stack_spill():
     """The BVH traversal stack keeps its newest entries in LDS and spills
     older ones to device memory when it runs deep.  A smaller LDS share

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <array>
 #include <random>
 #include <vector>
 
@@ -214,14 +215,54 @@ int main(int argc, char **argv) {
     }
     int n = argc > 1 ? atoi(argv[1]) : 1000;
     int seed = argc > 2 ? atoi(argv[2]) : 1;
-    int mode = argc > 3 ? atoi(argv[3]) : 0;   // 0 random, 1 all coincident, 2 a line
+    int mode = argc > 3 ? atoi(argv[3]) : 0;   // 0 random, 1 all coincident, 2 a line, 3 geometric spacing
     std::mt19937 rng(seed);
     std::uniform_real_distribution<float> U(-20, 20), S(0.1f, 2.0f);
     std::vector<Prim> P(n);
+    if (mode == 4) {   // spheres "cx cy cz r" from stdin (eye at the origin): the device tree's worst-case stack
+        P.clear();
+        std::vector<std::array<float, 4>> S;
+        float c[3], r;
+        double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, mag = 0;
+        while (scanf("%f %f %f %f", &c[0], &c[1], &c[2], &r) == 4) {
+            S.push_back({c[0], c[1], c[2], r});
+            for (int k = 0; k < 3; k++) {
+                lo[k] = std::min(lo[k], (double)c[k] - r), hi[k] = std::max(hi[k], (double)c[k] + r);
+                mag = std::max(mag, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
+            }
+        }
+        // distance bound and padding as build_bvh (rt_kernels.hip)
+        double diag2 = 0, far2 = 0;
+        for (int k = 0; k < 3; k++) {
+            diag2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);
+            double m = std::max(std::fabs(lo[k]), std::fabs(hi[k]));
+            far2 += m * m;
+        }
+        const double D = std::max(std::sqrt(diag2), std::sqrt(far2)) + mag + 1.0;
+        for (auto &q4 : S) {
+            Prim q;
+            double rr = std::sqrt((double)q4[3] * q4[3] + std::ldexp(D * D, -18)) + std::ldexp(D, -16);
+            for (int k = 0; k < 3; k++)
+                q.box.lo[k] = (float)(q4[k] - rr), q.box.hi[k] = (float)(q4[k] + rr), q.c[k] = q4[k];
+            q.cost = 1.0f;
+            q.key = (int)P.size();
+            P.push_back(q);
+        }
+        Result R1;
+        Builder B1(P);
+        B1.max_leaf = 1;
+        B1.trav_cost = 0.5f;
+        if (!B1.build(R1)) { printf("FAIL depth\n"); return 1; }
+        ResultW<4> Q;
+        collapse_sah<4>(R1, Q, 8, 0.5f);
+        printf("spheres=%zu nodes=%zu depth=%d stack=%d\n", P.size(), Q.nodes.size(), Q.depth, Q.max_stack);
+        return 0;
+    }
     for (int i = 0; i < n; i++) {
         float c[3] = {U(rng), U(rng), U(rng)};
         if (mode == 1) c[0] = c[1] = c[2] = 1.0f;
         if (mode == 2) c[0] = (float)i, c[1] = c[2] = 0.0f;
+        if (mode == 3) c[0] = std::pow(1.25f, (float)(i % 90)), c[1] = (float)(i / 90), c[2] = 0.0f;   // skewed: deep trees
         float r = S(rng);
         for (int k = 0; k < 3; k++) P[i].box.lo[k] = c[k] - r, P[i].box.hi[k] = c[k] + r, P[i].c[k] = c[k];
         P[i].cost = (i & 1) ? 3.0f : 1.0f;
