@@ -207,7 +207,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * launch timeline (100 MHz ticks): [24] first wave start, [26] last wave end;
  * RT_PROF builds also [25] work counter drained, [27] sum of per-wave tails, [28] sum of wave
  * lifetimes, [29] waves; [32] known-zero shadow rays, [33] brute-force queries, [34] stack
- * spills (as in rt_stats).  n <= 40. */
+ * spills (as in rt_stats), [35] BVH queries with a NaN origin or direction
+ * (no hit; not searched).  n <= 40. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

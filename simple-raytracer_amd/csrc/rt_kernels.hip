@@ -461,6 +461,16 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
     // directional shadow ray in a scene with spheres: this pass tests the
     // faces only, the spheres come in the point pass
     const bool faces_only = !point && !q.closest && !q.skipchk && q.unb && p.dir_bf == 2;
+    // A ray with a NaN in its origin or direction meets nothing in the
+    // reference (every distance and barycentric comparison is false): "no
+    // hit", mask unchanged, no SKIP.  The slab test would enter every box
+    // (fmaxf/fminf drop NaN) -- a whole-tree traversal.  (The cone pass
+    // rejects such a ray at its root: its cone tests are comparisons.)
+    if (!point && (__builtin_isnan(q.o.x) | __builtin_isnan(q.o.y) | __builtin_isnan(q.o.z) |
+                   __builtin_isnan(q.d.x) | __builtin_isnan(q.d.y) | __builtin_isnan(q.d.z))) {
+        atomicAdd(&p.stats[35], 1ull);
+        return;
+    }
     float best = q.tmax;                       // closest: running min (kFltMax at start)
     int win = -1;
     bool opaque = false;

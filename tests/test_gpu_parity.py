@@ -446,6 +446,28 @@ def _deep_scene_text(w: int = 32, h: int = 32) -> str:
     return "".join(out)
 
 
+def test_nan_rays_on_the_bvh():
+    """Rays with a NaN origin or direction (test7's and Test1's eta = 0
+    materials produce them) meet nothing in the reference; the
+    BVH answers them without a search (a NaN slab test would enter every box).
+    On the BVH path (accel = 1) the image matches the oracle, NaN pixels
+    included, with identical ray counts, and such queries did occur."""
+    seen = 0
+    for name in ("test7_s.txt", "Test1_s.txt"):
+        hs = rtamd.HostScene(name, cwd=SCENES)
+        W, H = hs.width, hs.height
+        gs = rtamd.GpuScene(hs)
+        gs.set_option("accel", 1)
+        img, st = gs.render_rows(hs.camera(), W, H, 0, H)
+        nan_q = gs.debug_counters()[35]
+        ref, cnt = OracleScene(name, cwd=SCENES).render()
+        assert_parity(img, ref, f"{name} accel1")
+        assert _counts(st) == cnt
+        seen += nan_q
+        _summary[f"nan_rays_{name}"] = dict(nan_queries=nan_q, nan_px=int(np.isnan(img).any(-1).sum()))
+    assert seen > 0
+
+
 def test_deep_stack_tree(tmp_path):
     """The stack spill area is sized per tree (Params::ovf_stride, from the
     deepest of the main and cone trees).  A skewed tree whose worst-case stack

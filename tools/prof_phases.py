@@ -40,6 +40,7 @@ def main():
     d = tempfile.mkdtemp(prefix="rtprof_")
     path = gen.write_scene(d, cfg, **kw)
     hs = rtamd.HostScene(path, cwd=d)
+    hs.set_depth(gen.CONFIGS[cfg]["depth"])          # the config's depth (C5: 8), as bench.py
     gs = rtamd.GpuScene(hs)
     for k, v in opts.items():
         gs.set_option(k, int(v))
