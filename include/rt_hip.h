@@ -208,7 +208,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * RT_PROF builds also [25] work counter drained, [27] sum of per-wave tails, [28] sum of wave
  * lifetimes, [29] waves; [32] known-zero shadow rays, [33] brute-force queries, [34] stack
  * spills (as in rt_stats), [35] BVH queries with a NaN origin or direction
- * (no hit; not searched).  n <= 40. */
+ * (no hit; not searched); RT_PROF builds: [36..38] traversal trips of primary /
+ * shadow / refraction + reflection queries.  n <= 40. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

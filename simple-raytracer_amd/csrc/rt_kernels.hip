@@ -317,6 +317,7 @@ struct Counters {
     unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
 #if RT_PROF
     unsigned trips;                             // traversal loop iterations of this lane
+    unsigned trips_kind[3];                     // ... of primary / shadow / refraction + reflection queries
 #endif
 #if RT_PROF >= 2
     unsigned long long t_fetch, t_trip;         // inner-node trips: cycles to node data, whole trip
@@ -429,6 +430,62 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
     }
 }
 
+// The six plane distances of a 4-wide node's children (rt_bvh.h Node4H):
+// plane a of child i at origin_a + h * 2^e_a (h binary16), i.e.
+// t = h * (2^e_a / d_a) + (origin_a - o_a) / d_a = fma(h, A_a, B_a) -- one
+// v_fma_mix_f32 per plane (h converted inside the fma, exactly); the rounding
+// (~ulp(D) in distance) is far inside the primitive padding.  (i, o) =
+// (1 / d, o / d) per axis, or (1, o) for a point query: then the planes are
+// the children's offsets from o.  Near / far plane per axis by the ray's
+// octant: t(h) is monotonic in h with the sign of A (= the sign of 1/d), so
+// min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10.
+struct ChildPlanes {
+    float tn[3][4], tf[3][4];                   // [axis][child]: near / far plane
+};
+__device__ __forceinline__ ChildPlanes child_planes(float4 w0, float4 w1, float4 w2, float4 w3, float ix, float iy,
+                                                    float iz, float ox, float oy, float oz, bool neg_x, bool neg_y,
+                                                    bool neg_z) {
+    // 2^e * (1/d): exact power-of-two scaling (one v_bfe_i32 + v_ldexp per
+    // axis; signed exponents in bytes 0..2 of w0.w), finite by the caps
+    const int ex = __float_as_int(w0.w);
+    const float A[3] = {__builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8)),
+                        __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8)),
+                        __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8))};
+    const float B[3] = {fmaf(w0.x, ix, -ox), fmaf(w0.y, iy, -oy), fmaf(w0.z, iz, -oz)};
+    // lower / upper bounds per axis, two children per word
+    const unsigned lo[3][2] = {{__float_as_uint(w1.x), __float_as_uint(w1.y)},
+                               {__float_as_uint(w1.z), __float_as_uint(w1.w)},
+                               {__float_as_uint(w2.x), __float_as_uint(w2.y)}};
+    const unsigned hi[3][2] = {{__float_as_uint(w2.z), __float_as_uint(w2.w)},
+                               {__float_as_uint(w3.x), __float_as_uint(w3.y)},
+                               {__float_as_uint(w3.z), __float_as_uint(w3.w)}};
+    const bool neg[3] = {neg_x, neg_y, neg_z};
+    ChildPlanes cp;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const h2v n = __builtin_bit_cast(h2v, neg[a] ? hi[a][j] : lo[a][j]);
+            const h2v f = __builtin_bit_cast(h2v, neg[a] ? lo[a][j] : hi[a][j]);
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                cp.tn[a][2 * j + e] = fmaf((float)n[e], A[a], B[a]);
+                cp.tf[a][2 * j + e] = fmaf((float)f[e], A[a], B[a]);
+            }
+        }
+    }
+    return cp;
+}
+
+// Entry distance of a ray into child i within [tlo, thi]: +inf for a miss or
+// an empty slot (unused slots link to the empty leaf, kEmptyLeaf: entering one
+// is harmless, so no link test; their inverted boxes miss anyway).
+__device__ __forceinline__ float child_entry(const ChildPlanes &cp, int i, float tlo, float thi) {
+    const float tn = fmaxf(fmaxf(cp.tn[0][i], cp.tn[1][i]), fmaxf(cp.tn[2][i], tlo));
+    const float tf = fminf(fminf(cp.tf[0][i], cp.tf[1][i]), fminf(cp.tf[2][i], thi));
+    return (tn <= tf) ? tn : kInf;
+}
+
 // stk: this lane's traversal stack in LDS (entries kBlock apart).
 //
 // While-while traversal with speculative leaf postponement (Aila & Laine
@@ -509,64 +566,30 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
         }
         return n;
     };
-    // One 4-wide node (rt_bvh.h Node4H): plane a of child i at origin_a +
-    // h * 2^e_a (h binary16), i.e. t = h * (2^e_a / d_a) + (origin_a - o_a) / d_a
-    // = fma(h, A_a, B_a) -- one v_fma_mix_f32 per plane (h converted inside
-    // the fma, exactly); the rounding (~ulp(D) in distance) is far inside the
-    // primitive padding.  Slab-test the children, push the far hits, continue
-    // with the nearest, park the first leaf reached.
+    // One 4-wide node (rt_bvh.h Node4H, child_planes): slab-test the
+    // children, push the far hits, continue with the nearest, park the first
+    // leaf reached.
     auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3, float4 w4) {
 #if RT_PROF
         cnt.trips++;
 #endif
         cnt.boxes += 4;
         float thi = thi_now();
-        // 2^e * (1/d): exact power-of-two scaling (one v_bfe_i32 + v_ldexp per
-        // axis; signed exponents in bytes 0..2 of w0.w), finite by the caps
-        const int ex = __float_as_int(w0.w);
-        float Ax = __builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8));
-        float Ay = __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8));
-        float Az = __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8));
-        float Bx = fmaf(w0.x, ix, -ox), By = fmaf(w0.y, iy, -oy), Bz = fmaf(w0.z, iz, -oz);
-        // lower / upper bounds per axis, two children per word
-        const unsigned lx[2] = {__float_as_uint(w1.x), __float_as_uint(w1.y)};
-        const unsigned ly[2] = {__float_as_uint(w1.z), __float_as_uint(w1.w)};
-        const unsigned lz[2] = {__float_as_uint(w2.x), __float_as_uint(w2.y)};
-        const unsigned hx[2] = {__float_as_uint(w2.z), __float_as_uint(w2.w)};
-        const unsigned hy[2] = {__float_as_uint(w3.x), __float_as_uint(w3.y)};
-        const unsigned hz[2] = {__float_as_uint(w3.z), __float_as_uint(w3.w)};
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
-        // near / far plane per axis by the ray's octant: t(h) = fma(h, A, B) is
-        // monotonic in h with the sign of A (= the sign of 1/d), so
-        // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10
-        h2v nx[2], fx[2], ny[2], fy[2], nz[2], fz[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            nx[j] = __builtin_bit_cast(h2v, neg_x ? hx[j] : lx[j]), fx[j] = __builtin_bit_cast(h2v, neg_x ? lx[j] : hx[j]);
-            ny[j] = __builtin_bit_cast(h2v, neg_y ? hy[j] : ly[j]), fy[j] = __builtin_bit_cast(h2v, neg_y ? ly[j] : hy[j]);
-            nz[j] = __builtin_bit_cast(h2v, neg_z ? hz[j] : lz[j]), fz[j] = __builtin_bit_cast(h2v, neg_z ? lz[j] : hz[j]);
-        }
+        const ChildPlanes cp = child_planes(w0, w1, w2, w3, ix, iy, iz, ox, oy, oz, neg_x, neg_y, neg_z);
         float k[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int j = i / 2, e = i % 2;
-            float tnx = fmaf((float)nx[j][e], Ax, Bx), tfx = fmaf((float)fx[j][e], Ax, Bx);
-            float tny = fmaf((float)ny[j][e], Ay, By), tfy = fmaf((float)fy[j][e], Ay, By);
-            float tnz = fmaf((float)nz[j][e], Az, Bz), tfz = fmaf((float)fz[j][e], Az, Bz);
             if (!point) {
-                float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tlo));
-                float tf = fminf(fminf(tfx, tfy), fminf(tfz, thi));
-                // entry distance of a hit child, +inf for a miss or an empty
-                // slot (unused slots link to the empty leaf, kEmptyLeaf:
-                // entering one is harmless, so no link test; their inverted
-                // boxes miss anyway)
-                k[i] = (tn <= tf) ? tn : kInf;
+                k[i] = child_entry(cp, i, tlo, thi);
             } else {
                 // shadow cone (see dir_tree): the child's box lies at offsets
                 // [tn, tf] from the origin po, z along the light; it may hold
                 // a shadowing sphere iff its top is not below po and its
                 // lateral distance d satisfies d^2 <= cone_k * top^2 (and,
                 // for a bounded region, its bottom is within cone_h)
+                const float tnx = cp.tn[0][i], tny = cp.tn[1][i], tnz = cp.tn[2][i];
+                const float tfx = cp.tf[0][i], tfy = cp.tf[1][i], tfz = cp.tf[2][i];
                 float dx = fmaxf(fmaxf(tnx, -tfx), 0.0f), dy = fmaxf(fmaxf(tny, -tfy), 0.0f);
                 float d2 = fmaf(dx, dx, dy * dy);
                 bool in = (tfz >= 0.0f) & (d2 <= cone_k * (tfz * tfz)) & (tnz <= cone_h);
@@ -1256,6 +1279,14 @@ __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, 
     y = (int)s * 8 + (int)(r % (unsigned)sh);
 }
 
+// Primary ray of local pixel (x, y): p = ul + dh * x + dv * row, direction
+// (p - eye).norm() (main.cpp:720-728, that association order)
+__device__ __forceinline__ V3 primary_dir(const Params &p, int x, int y) {
+    V3 pt = vadd(vadd(V3{p.ul[0], p.ul[1], p.ul[2]}, vmul(V3{p.dh[0], p.dh[1], p.dh[2]}, (float)x)),
+                 vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)image_row(p, y)));
+    return vnorm(vsub(pt, V3{p.eye[0], p.eye[1], p.eye[2]}));
+}
+
 template <int MAXF, int MODE>
 __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) {
     constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
@@ -1293,6 +1324,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #if RT_PROF
     cnt.trips = 0;
+    cnt.trips_kind[0] = cnt.trips_kind[1] = cnt.trips_kind[2] = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
     unsigned long long t_drain = 0;
 #endif
@@ -1333,11 +1365,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     unsigned idx = base + rank;
                     if (idx < p.total) {
                         pixel_xy(p, idx, px, py);
-                        V3 pt = vadd(vadd(V3{p.ul[0], p.ul[1], p.ul[2]}, vmul(V3{p.dh[0], p.dh[1], p.dh[2]}, (float)px)),
-                                     vmul(V3{p.dv[0], p.dv[1], p.dv[2]}, (float)image_row(p, py)));
-                        V3 eye = {p.eye[0], p.eye[1], p.eye[2]};
-                        q.o = eye;
-                        q.d = vnorm(vsub(pt, eye));
+                        q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
+                        q.d = primary_dir(p, px, py);
                         q.tmin = 0.0f;               // primary rays accept any t > 0 (main.cpp:736)
                         q.tmax = kFltMax;
                         q.unb = false;
@@ -1415,6 +1444,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             }
 #if RT_PROF
             int d = (int)(cnt.trips - tr0);
+            cnt.trips_kind[kind == RK_PRIMARY ? 0 : kind == RK_SHADOW ? 1 : 2] += (unsigned)d;
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
             pc_wtrips += (unsigned long long)d;
             unsigned long long c2 = __builtin_amdgcn_s_memtime();
@@ -1460,6 +1490,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[14], pc_wtrips);
     }
     atomicAdd(&st[15], (unsigned long long)cnt.trips);
+    atomicAdd(&st[36], (unsigned long long)cnt.trips_kind[0]);
+    atomicAdd(&st[37], (unsigned long long)cnt.trips_kind[1]);
+    atomicAdd(&st[38], (unsigned long long)cnt.trips_kind[2]);
     if (lane == 0) {
         if (!t_drain) t_drain = t_end;
         atomicMin(&st[25], t_drain);                 // work counter ran out

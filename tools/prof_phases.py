@@ -74,6 +74,7 @@ def main():
                         if c[29] else None),
         "inner_trip_cycles": ({"fetch": c[30] / max(1, c[6] // 4), "trip": c[31] / max(1, c[6] // 4)}
                               if c[31] else None),
+        "lane_trips_by_kind": dict(zip(["primary", "shadow", "refr_refl"], c[36:39])),
         "raw": c,
     }
     print(json.dumps(res, indent=1))
