@@ -46,5 +46,6 @@ d["dram_read_req_frac"] = g("TCC_EA0_RDREQ_DRAM_sum") / g("TCC_EA0_RDREQ_sum")
 d["dram_write_req_frac"] = g("TCC_EA0_WRREQ_DRAM_sum") / g("TCC_EA0_WRREQ_sum")
 d["l1_read_miss_frac"] = g("TCP_TCC_READ_REQ_sum") / g("TCP_TOTAL_READ_sum")
 d["l1_to_l2_read_latency_cyc"] = g("TCP_TCC_READ_REQ_LATENCY_sum") / g("TCP_TCC_READ_REQ_sum")
-out["derived"] = d
+# counters not collected in this run: left out (strict JSON has no NaN)
+out["derived"] = {k: v for k, v in d.items() if v is not None and v == v}
 print(json.dumps(out, indent=1))
