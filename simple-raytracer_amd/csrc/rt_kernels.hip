@@ -789,7 +789,9 @@ template <int MAXF>
 struct Cold {
     float4 saved[4];                 // the node's LDS state while a child runs
     float P[3];                      // its hit point (incidence_object_intersection.point)
-    int stack[MAXF];                 // medium stack (incident_object_stack), object indices
+    int stack[MAXF];                 // the CHILD's medium stack (incident_object_stack), object indices:
+                                     // written with the node's own state when it opens the child, so
+                                     // one frame line is dirtied per child open, not two
     int pad_[(MAXF + 3 + 15) / 16 * 16 - (MAXF + 3)];
 };
 static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17>) == 192, "cold frame sizes");
@@ -914,6 +916,20 @@ __device__ __forceinline__ bool in_stack(const Cold<MAXF> &f, int sn, int obj) {
     return in;
 }
 
+// The parent's medium stack into the child's (frame fc holds the parent's,
+// c the child's: the frames one level up).  The root node's (level 0, a
+// primary hit) is always {its own object} (main.cpp:751-757) and lives in no
+// frame.
+template <int MAXF>
+__device__ __forceinline__ void copy_stack(const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, bool root) {
+    if (root) {
+        c.stack[0] = f.obj;
+    } else {
+        const int fsn = h_sn(f);
+        for (int q = 0; q < fsn; q++) c.stack[q] = fc.stack[q];
+    }
+}
+
 // The child's medium state after a transition: state, stack size, eta_i, eta_t
 // (its stack is written into the child's cold frame).
 struct Medium {
@@ -972,9 +988,9 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
 template <int MAXF>
 __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
-                                  Counters &cnt) {
+                                  bool root, Counters &cnt) {
     const int fsn = h_sn(f);
-    for (int q = 0; q < fsn; q++) c.stack[q] = fc.stack[q];
+    copy_stack(f, fc, c, root);
     int n = fsn;
     Medium m;
     float hit_eta = p.objs[hit].eta;
@@ -997,7 +1013,7 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
             c.stack[n++] = hit;
         }
     } else if (n > 0) {
-        if (!in_stack(fc, fsn, hit)) {
+        if (!(root ? hit == f.obj : in_stack(fc, fsn, hit))) {
             m.state = ENTERING;
             m.ei = f.et;
             m.et = hit_eta;
@@ -1021,9 +1037,10 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
 
 // Medium-stack transition for the reflection child (main.cpp:1134-1182).
 template <int MAXF>
-__device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit) {
+__device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
+                                  bool root) {
     const int fsn = h_sn(f);
-    for (int q = 0; q < fsn; q++) c.stack[q] = fc.stack[q];
+    copy_stack(f, fc, c, root);
     int n = fsn;
     Medium m;
     float hit_eta = p.objs[hit].eta;
@@ -1031,7 +1048,7 @@ __device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAX
         m.state = ENTERING;
         m.ei = f.ei;
         if (n > 0) {
-            if (!in_stack(fc, fsn, hit)) {
+            if (!(root ? hit == f.obj : in_stack(fc, fsn, hit))) {
                 m.et = hit_eta;
                 c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
             } else {
@@ -1123,8 +1140,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             color = bkg;
             return RK_NONE;
         }
-        m = Medium{ENTERING, 1, p.eta_bkg, p.objs[q.win].eta};
-        ls.cold()[0].stack[0] = q.win;
+        m = Medium{ENTERING, 1, p.eta_bkg, p.objs[q.win].eta};   // stack {q.win}: implicit (copy_stack)
         open = true;
         top = 0;
     } else {
@@ -1167,7 +1183,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 cnt.skip++;                          // tmp_transparency stays 0
                 set_phase(h, PH_REFL);
             } else if (q.win >= 0) {
-                m = refr_transition(p, h, ls.cold()[top], ls.cold()[top + 1], q.win, cnt);
+                m = refr_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0, cnt);
                 set_phase(h, PH_REFR_CHILD);
                 open = true;
             } else {
@@ -1178,7 +1194,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             }
         } else {                                     // PH_REFL
             if (q.win >= 0) {
-                m = refl_transition(p, h, ls.cold()[top], ls.cold()[top + 1], q.win);
+                m = refl_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0);
                 set_phase(h, PH_REFL_CHILD);
                 open = true;
             } else {
@@ -1221,7 +1237,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 closest_query(q, p, T);
                 const int sn = h_sn(h);
                 q.skipchk = (sn > 0) && !ob.is_sphere;
-                q.back = sn > 0 ? ls.cold()[top].stack[sn - 1] : -1;
+                q.back = sn > 0 ? (top == 0 ? h.obj : ls.cold()[top - 1].stack[sn - 1]) : -1;
                 set_phase(h, PH_REFR);
                 lds_store_phase(h);
                 ls.top = top;
