@@ -4,18 +4,21 @@
 // The reference scans every primitive for every ray (TraceRay, main.cpp:1218-
 // 1403).  The BVH only decides WHICH primitives a ray can possibly hit; every
 // candidate is still tested with the reference's exact formulas, and the
-// device traversal reproduces the reference's visiting order where it matters
-// (closest-hit ties, shadow-mask product order).  For that the
-// boxes must be conservative for the *computed* intersections, which deviate
-// from exact geometry by rounding:
+// device traversal answers the reference's order-dependent cases exactly
+// (closest-hit ties, SKIP_TRANS).  For that the boxes must
+// be conservative for the *computed* intersections, which deviate from exact
+// geometry by rounding (build_bvh in rt_kernels.hip pads the primitives):
 //   face:   the accepted hit point is within a few ulp(scene scale) of the
-//           triangle -> pad by 2^-14 * D * cond(triangle), cond = |e1|^2|e2|^2/det
+//           triangle -> pad by 2^-16 * D * max(1, cond), cond = |e1|^2|e2|^2/det
+//           (32x the rounding bound of the barycentric test)
 //   sphere: the discriminant B^2 - 4C is computed with absolute error up to
-//           ~2^-18.4 D^2 (|dir| <= D), so rays up to sqrt(r^2 + 2^-18 D^2) from
-//           the centre can be "hits" -> radius grown accordingly
+//           ~2^-18.4 D^2 (|dir| <= D), so rays up to sqrt(r^2 + 2^-20 D^2) from
+//           the centre can be "hits" -> radius grown to sqrt(r^2 + 2^-18 D^2)
+//           + 2^-16 D (a factor 4 of margin on the error term)
 // where D bounds the distance from any ray origin (eye or a surface point) to
 // any primitive.  (The directional-light sphere quirk -- A = 1 assumed for an
-// unnormalised direction -- is not geometric at all; those rays bypass the BVH.)
+// unnormalised direction -- is not ray geometry: those shadow rays query a
+// per-light cone tree over the spheres, dir_tree in rt_kernels.hip.)
 #pragma once
 
 #include <algorithm>
