@@ -119,6 +119,7 @@ struct LightK {
     float L[3], pad1;         // directional: light.direction.norm() * -1 (main.cpp:887)
     float sdir[3], pad2;      // directional: light.direction * -1 (main.cpp:895, unnormalised)
 };
+static_assert(sizeof(LightK) % sizeof(float4) == 0, "lights are staged in LDS as float4s");
 struct TexK {
     int w, h;
     long long off;                       // first byte in Params::texels
@@ -161,6 +162,7 @@ struct Params {
     const DirK *__restrict__ dirk;       // per light (dir_bf == 2)
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int ovf_stride;                      // BVH: stack spill entries per lane (deepest tree, kSpill multiple)
+    int lights_lds;                      // the lights' copy in LDS: float4 offset in rt_lds
     int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
     void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
     int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
@@ -745,7 +747,14 @@ enum {
     LW_N = 0, LW_I = 3, LW_DIF = 6, LW_ACC = 9, LW_OBJ = 12, LW_META = 13, LW_EI = 14, LW_ET = 15,
     kLdsHot = 16
 };
-extern __shared__ float4 rt_lds[];   // dynamic LDS of render_kernel: state, then stack / primitives
+extern __shared__ float4 rt_lds[];   // dynamic LDS of render_kernel: state, then stack / primitives, lights
+
+// The lights, staged in LDS at kernel start: a shading step's light reads are
+// then LDS latency, not a dependent trip to L2 (one dependent load per
+// shading step costs ~1 % of C3, profiles/r02/ab_shading_probe.txt)
+__device__ __forceinline__ const LightK *lds_lights(const Params &p) {
+    return reinterpret_cast<const LightK *>(rt_lds + p.lights_lds);
+}
 
 __device__ __forceinline__ float *lane_lds() { return reinterpret_cast<float *>(rt_lds) + threadIdx.x; }
 __device__ __forceinline__ int h_light_lds() { return (int)(__float_as_uint(lane_lds()[LW_META * kBlock]) >> 9); }
@@ -1096,7 +1105,7 @@ __device__ __forceinline__ void shadow_query(Query &q, const Params &p, int ligh
     V3 L, sd;
     float dl;
     bool unb;
-    light_vectors(p.lights[light], q.o, L, sd, dl, unb);
+    light_vectors(lds_lights(p)[light], q.o, L, sd, dl, unb);
     q.d = sd;
     q.tmin = p.eps;
     q.tmax = dl;
@@ -1149,7 +1158,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
             const int light = h_light(h);
             // the light's words in one batch (LightK: xyz w | col | L)
-            const f4v *lw = reinterpret_cast<const f4v *>(p.lights + light);
+            const f4v *lw = reinterpret_cast<const f4v *>(lds_lights(p) + light);
             const f4v lw0 = lw[0], lw1 = lw[1], lw2 = lw[2];
             // L as light_vectors computed it for the shadow ray just traced:
             // that ray's direction for a point light, the constant -L for a
@@ -1315,8 +1324,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         int nf4 = 5 * p.nf, ns4 = p.ns;
         for (int i = threadIdx.x; i < nf4; i += blockDim.x) lds[i] = p.fscan[i];
         for (int i = threadIdx.x; i < ns4; i += blockDim.x) lds[nf4 + i] = p.sscan[i];
-        __syncthreads();
     }
+    {
+        const int nl4 = p.nl * (int)(sizeof(LightK) / sizeof(float4));
+        const float4 *src = reinterpret_cast<const float4 *>(p.lights);
+        for (int i = threadIdx.x; i < nl4; i += blockDim.x) rt_lds[p.lights_lds + i] = src[i];
+    }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     LaneState<MAXF> ls;
     ls.top = -1;
@@ -1632,11 +1646,16 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
 
 V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
-size_t mode_lds_bytes(const rt_scene *s, int mode) {
+// Dynamic LDS of render_kernel: the per-lane shading state, the mode's region
+// (BVH stacks or the staged primitives), then the lights.
+size_t mode_region_end(const rt_scene *s, int mode) {
     size_t shade = (size_t)kLdsHot * kBlock * sizeof(float);         // per-lane shading state
     if (mode == MODE_SCAN_LDS) return shade + s->lds_bytes;
     if (mode == MODE_BVH) return shade + (size_t)s->base.stack_cap * kBlock * sizeof(int);
     return shade;
+}
+size_t mode_lds_bytes(const rt_scene *s, int mode) {
+    return mode_region_end(s, mode) + (size_t)s->base.nl * sizeof(LightK);
 }
 
 template <int MAXF, int MODE>
@@ -1650,6 +1669,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
     Params pl = p;
+    pl.lights_lds = (int)(mode_region_end(s, MODE) / sizeof(float4));
     const size_t cold_bytes = (size_t)grid * kBlock * MAXF * sizeof(Cold<MAXF>);
     size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
     if (slot.frames_cap < fbytes) {
