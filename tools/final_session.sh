@@ -26,4 +26,9 @@ step pmc_sq timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CY
 step pmc_sq2 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_THREAD_CYCLES_VALU TA_BUSY_avr -d $O/pmc/p4 -o run --output-format csv -- python3 bench.py --cpu-baseline off --steps 1 --warmup 0 --inflight 1
 step pmc_tcc timeout -k 10 300 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d $O/pmc/p5 -o run --output-format csv -- python3 bench.py --cpu-baseline off --steps 1 --warmup 0 --inflight 1
 RENDERS=2 python3 tools/pmc_summary.py $O/pmc > $O/C3_pmc.json
+if [ -d simple-raytracer_amd/lib_prof ]; then   # RT_PROF build: make VARIANT=prof EXTRA=-DRT_PROF=1
+  for c in C3 C5; do
+    step phases_$c bash -c "RTAMD_LIB_DIR=simple-raytracer_amd/lib_prof timeout -k 10 300 python tools/prof_phases.py $c > $O/phases_$c.json 2> $O/phases_$c.err"
+  done
+fi
 echo done
