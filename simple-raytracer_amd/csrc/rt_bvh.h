@@ -89,7 +89,6 @@ struct NodeW {
     int32_t pad[3];
 };
 using Node4 = NodeW<4>;
-using Node8 = NodeW<8>;
 static_assert(sizeof(Node4) == 128, "node4 layout");
 
 template <int W>
@@ -99,7 +98,6 @@ struct ResultW {
     int max_stack = 0;       // worst-case entries a near-first traversal pushes
 };
 using Result4 = ResultW<4>;
-using Result8 = ResultW<8>;
 
 // Collapse a binary tree (Result) into W-wide nodes.
 template <int W>
@@ -160,7 +158,6 @@ inline void collapse(const Result &R, ResultW<W> &Q) {
     conv(0, 1, 0);
     Q.nodes[0].max_stack = Q.max_stack;
 }
-inline void collapse4(const Result &R, Result4 &Q) { collapse<4>(R, Q); }
 
 // SAH-optimal collapse (Ylitie et al. 2017, §3.1).  Over the binary tree,
 // C(n, i) is the least SAH cost of covering subtree n with at most i units,
