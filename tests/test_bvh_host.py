@@ -20,7 +20,26 @@ def checker(tmp_path_factory):
 
 
 @pytest.mark.parametrize("n,seed,mode", [(1, 1, 0), (2, 1, 0), (3, 2, 0), (17, 3, 0), (1000, 4, 0),
-                                         (2000, 5, 0), (100000, 6, 0), (500, 7, 1), (5000, 8, 2)])
+                                         (2000, 5, 0), (100000, 6, 0), (500, 7, 1), (5000, 8, 2), (900, 9, 3)])
 def test_bvh_structure(checker, n, seed, mode):
+    """Greedy and SAH-optimal collapses, binary16 node bounds (containment and
+    one-step tightness), leaf records -- on random, coincident, collinear and
+    geometrically spaced (deep) primitive sets."""
     r = subprocess.run([checker, str(n), str(seed), str(mode)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+def test_bvh_device_padding_stack(checker):
+    """Mode 4 builds the device's tree (sphere padding of build_bvh, SAH
+    collapse) from sphere centres on stdin and reports its worst-case stack:
+    the deep-stack GPU test's scene gives a skewed tree."""
+    import math
+    lines = []
+    for i in range(800):
+        k, arm = i % 200, i // 200
+        d, ang = 1.08 ** k, arm * math.pi / 2
+        lines.append(f"{math.cos(ang) * d * 0.3} {math.sin(ang) * d * 0.3} {-(5 + d)} 0.4")
+    r = subprocess.run([checker, "0", "0", "4"], input="\n".join(lines), capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.startswith("spheres=800"), r.stdout + r.stderr
+    stack = int(r.stdout.split("stack=")[1].split()[0])
+    assert stack >= 24, r.stdout
