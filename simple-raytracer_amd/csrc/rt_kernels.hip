@@ -187,6 +187,7 @@ constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading
 constexpr int kSpill = 8;
 static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack - 3 > kSpill, "stack spill blocks");
 constexpr int kBlock = 256;
+constexpr unsigned kChunk = 64;          // work items a wave takes at a time: one 8x8 tile (pixel_xy)
 
 // ---------------------------------------------------------------------------
 // One lane's ray query (a TraceRay call + the consumer loop that follows it)
@@ -1344,6 +1345,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
     bool drained = false;      // wave saw the work counter run out
+    unsigned chunk_pos = 0, chunk_end = 0;   // the wave's tile: its unused work items [pos, end)
     int px = 0, py = 0;
 #if RT_PROF >= 2
     cnt.t_fetch = cnt.t_trip = 0;
@@ -1381,18 +1383,32 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             if (idle) {
                 unsigned n = (unsigned)__popcll(idle);
                 int leader = __ffsll((long long)idle) - 1;
-                unsigned base = 0;
-                if (lane == leader) base = atomicAdd(p.work, n);
-                base = __shfl(base, leader);
-                if (base + n >= p.total) {
-                    drained = true;
-#if RT_PROF
-                    t_drain = __builtin_amdgcn_s_memrealtime();
-#endif
+                // The wave takes work a whole 8x8 tile (kChunk items) at a
+                // time and refills its lanes from it: a wave's lanes stay on
+                // neighbouring pixels, whose rays walk the same nodes (+3 %
+                // one frame, +4.5 % pipelined on C3 against taking exactly
+                // the idle lanes' count from the counter each time,
+                // profiles/r02/ab_chunk.txt).  Ranks < split take the rest of
+                // the current tile, the others the start of the next one.
+                const unsigned left = chunk_end - chunk_pos;
+                const unsigned base = chunk_pos, split = min(n, left);
+                unsigned nbase = 0;
+                if (n > left) {
+                    unsigned g = 0;
+                    if (lane == leader) g = atomicAdd(p.work, kChunk);
+                    nbase = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
+                    chunk_pos = nbase + (n - split);
+                    chunk_end = nbase + kChunk;
+                    if (nbase >= p.total) drained = true;
+                } else {
+                    chunk_pos += n;
                 }
+#if RT_PROF
+                if (drained) t_drain = __builtin_amdgcn_s_memrealtime();
+#endif
                 if (!busy) {
                     unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
-                    unsigned idx = base + rank;
+                    unsigned idx = rank < split ? base + rank : nbase + (rank - split);
                     if (idx < p.total) {
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
