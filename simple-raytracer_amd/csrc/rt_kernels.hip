@@ -1289,18 +1289,29 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
     }
 }
 
-// Pixel index -> (x, y): strips of 8 rows, 8x8 blocks along the strip, so a
-// wave's 64 consecutive indices cover an 8x8 tile.
 // image row of local row r (block-interleaved row sets for multi-GPU balance)
 __device__ __forceinline__ int image_row(const Params &p, int r) {
     return p.y0 + (r / p.rblock) * p.rstep + r % p.rblock;
 }
+
+// Pixel index -> (x, y): strips of 8 rows, 8x8 tiles along the strip, so a
+// wave's 64-index chunk is one tile. Inside a whole tile the indices run in Z
+// order, so the few lanes a wave refills at once get a compact 2x2 / 4x4 group
+// (+0.6 % on C3, every A/B round); a partial tile (W % 8, the last strip) keeps
+// column order. Both are bijections, so the image does not change.
 
 __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, int &y) {
     unsigned strip_px = (unsigned)p.W * 8u;
     unsigned s = idx / strip_px;
     unsigned r = idx - s * strip_px;
     int sh = min(8, p.rows - (int)s * 8);
+    const unsigned t = r >> 6;
+    if (sh == 8 && (int)(t * 8 + 8) <= p.W) {      // a whole 8x8 tile: Z order inside it
+        const unsigned rr = r & 63u;
+        x = (int)(t * 8 + ((rr & 1u) | ((rr >> 1) & 2u) | ((rr >> 2) & 4u)));
+        y = (int)s * 8 + (int)(((rr >> 1) & 1u) | ((rr >> 2) & 2u) | ((rr >> 3) & 4u));
+        return;
+    }
     x = (int)(r / (unsigned)sh);
     y = (int)s * 8 + (int)(r % (unsigned)sh);
 }
