@@ -164,6 +164,7 @@ struct Params {
     int ovf_stride;                      // BVH: stack spill entries per lane (deepest tree, kSpill multiple)
     int lights_lds;                      // the lights' copy in LDS: float4 offset in rt_lds
     int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
+    unsigned chunk;                      // work items a wave takes from the counter at a time (0: its idle lanes' count)
     void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
     int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
 };
@@ -187,7 +188,7 @@ constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading
 constexpr int kSpill = 8;
 static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack - 3 > kSpill, "stack spill blocks");
 constexpr int kBlock = 256;
-constexpr unsigned kChunk = 64;          // work items a wave takes at a time: one 8x8 tile (pixel_xy)
+constexpr unsigned kChunkDefault = 64;   // work items a wave takes at a time: one 8x8 tile (pixel_xy)
 
 // ---------------------------------------------------------------------------
 // One lane's ray query (a TraceRay call + the consumer loop that follows it)
@@ -1394,22 +1395,23 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             if (idle) {
                 unsigned n = (unsigned)__popcll(idle);
                 int leader = __ffsll((long long)idle) - 1;
-                // The wave takes work a whole 8x8 tile (kChunk items) at a
-                // time and refills its lanes from it: a wave's lanes stay on
-                // neighbouring pixels, whose rays walk the same nodes (+3 %
-                // one frame, +4.5 % pipelined on C3 against taking exactly
-                // the idle lanes' count from the counter each time,
-                // profiles/r02/ab_chunk.txt).  Ranks < split take the rest of
-                // the current tile, the others the start of the next one.
+                // The wave takes p.chunk work items at a time (a whole 8x8
+                // tile, or just its idle lanes' count when p.chunk = 0: see
+                // chunk_for) and refills its lanes from them: with tiles a
+                // wave's lanes stay on neighbouring pixels, whose rays walk
+                // the same nodes (profiles/r02/ab_chunk.txt).  Ranks < split
+                // take the rest of the current chunk, the others the start of
+                // the next one.
                 const unsigned left = chunk_end - chunk_pos;
                 const unsigned base = chunk_pos, split = min(n, left);
                 unsigned nbase = 0;
                 if (n > left) {
                     unsigned g = 0;
-                    if (lane == leader) g = atomicAdd(p.work, kChunk);
+                    const unsigned take = max(p.chunk, n - split);
+                    if (lane == leader) g = atomicAdd(p.work, take);
                     nbase = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
                     chunk_pos = nbase + (n - split);
-                    chunk_end = nbase + kChunk;
+                    chunk_end = nbase + take;
                     if (nbase >= p.total) drained = true;
                 } else {
                     chunk_pos += n;
@@ -1618,6 +1620,8 @@ struct rt_scene {
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
+    long long opt_chunk = -1;          // refill chunk (-1: by the scene, chunk_for)
+    bool secondary = false;            // some material reflects (ks > 0) or refracts (opacity < 1, eta > 0)
     long long opt_reserve = 0;         // occupancy-derived grid: block slots left free for other kernels
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
     long long opt_bvh_leaf = 8;        // SAH max leaf size
@@ -1685,6 +1689,17 @@ size_t mode_lds_bytes(const rt_scene *s, int mode) {
     return mode_region_end(s, mode) + (size_t)s->base.nl * sizeof(LightK);
 }
 
+// Work items a wave takes from the pixel counter at a time.  A whole 8x8 tile
+// (kChunkDefault) when pixels spawn reflection / refraction rays: the wave's
+// secondary rays then leave neighbouring points of the same surfaces (C3 +5 %,
+// C3G +4.5 %, C5 +9 % against 0).  With primary and shadow rays only, a wave
+// takes exactly its idle lanes' count: tiles measured C4 -16 %, C2 -6 %
+// (profiles/r02/ab_chunk_auto.txt).  The image does not depend on it.
+static unsigned chunk_for(const rt_scene *s, const Params &p) {
+    if (s->opt_chunk >= 0) return (unsigned)s->opt_chunk;
+    return s->secondary && p.depth > 0 ? kChunkDefault : 0u;
+}
+
 template <int MAXF, int MODE>
 hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_t st, bool dry) {
     size_t shm = mode_lds_bytes(s, MODE);
@@ -1696,6 +1711,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
     Params pl = p;
+    pl.chunk = chunk_for(s, p);
     pl.lights_lds = (int)(mode_region_end(s, MODE) / sizeof(float4));
     const size_t cold_bytes = (size_t)grid * kBlock * MAXF * sizeof(Cold<MAXF>);
     size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
@@ -2143,6 +2159,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
         o.tex = tex;
         o.is_sphere = is_sphere;
         ofac[k] = (float)(1.0 - (double)m.opacity);
+        if (m.ks > 0.0f || (m.opacity < 1.0f && m.eta > 0.0f)) s->secondary = true;
     };
     for (int i = 0; i < nf; i++) {
         const rt_face_desc &F = desc->faces[i];
@@ -2271,6 +2288,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.dir_bf = 0;                      // set with the BVH (build_bvh); the scan needs none
     p.shadow_early_out = nan_fac ? 0 : 1;
     p.stack_cap = kLdsStackDefault;
+    p.chunk = kChunkDefault;           // launch_one: chunk_for
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
     *out = s;
     return RT_OK;
@@ -2304,6 +2322,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "accel") s->opt_accel = value;
     else if (k == "inflight") return set_inflight(s, value);
     else if (k == "fail_bvh_upload") s->opt_fail_bvh_upload = value;
+    else if (k == "chunk") {
+        if (value < 0 || value > 4096) return RT_E_INVALID;
+        s->opt_chunk = value;
+    }
     else if (k == "lds_stack") {
         if (value < 12 || value > kLdsStack) return RT_E_INVALID;
         s->base.stack_cap = (int)value;

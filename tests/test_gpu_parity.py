@@ -511,6 +511,23 @@ def test_lds_stack_spill():
             gs.set_option("lds_stack", 11)
 
 
+def test_refill_chunk_bit_identical():
+    """How many work items a wave takes from the pixel counter at a time
+    (option chunk; by default a whole 8x8 tile when the scene spawns
+    reflection/refraction rays, else the idle lanes' count) decides which lane
+    renders which pixel, never a pixel's value: every chunk, including ones
+    that do not align with the 8x8 tiles and a ragged 37x23 image, gives the
+    same image and ray counts bit for bit."""
+    for name, size in (("C3_64x64.txt", None), ("C4_32x32.txt", None), ("test7_s.txt", (37, 23))):
+        ref, st = rtamd.render_scene(name, cwd=SCENES, imsize=size)
+        for c in (0, 1, 16, 64, 100, 256):
+            img, st2 = rtamd.render_scene(name, cwd=SCENES, imsize=size, options={"chunk": c})
+            assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, c)
+            assert _counts(st2) == _counts(st), (name, c)
+    with pytest.raises(rtamd.RTError):
+        rtamd.render_scene("test7_s.txt", cwd=SCENES, options={"chunk": -1})
+
+
 @pytest.mark.parametrize("opts", [{"bvh_collapse": 0}, {"bvh_collapse": 1, "bvh_node": 1000}])
 def test_bvh_collapse_parity(opts):
     """The 4-wide tree comes from the binary SAH tree by an SAH-optimal
