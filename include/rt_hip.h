@@ -196,6 +196,9 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * deeper stacks spill to device memory -- a test knob), "bvh_leaf",
  * "bvh_trav" (binary SAH: largest leaf, node cost x1000), "bvh_collapse"
  * (0 greedy, 1 SAH-optimal 4-wide collapse), "bvh_node" (its node cost x1000),
+ * "chunk" (0..4096: pixels a wave takes from the work counter at a time,
+ * 0 = as many as it has idle lanes; default: 64, one 8x8 tile, when some
+ * material reflects or refracts, else 0 -- never changes the image),
  * "fail_bvh_upload" (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
@@ -209,7 +212,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * lifetimes, [29] waves; [32] known-zero shadow rays, [33] brute-force queries, [34] stack
  * spills (as in rt_stats), [35] BVH queries with a NaN origin or direction
  * (no hit; not searched); RT_PROF builds: [36..38] traversal trips of primary /
- * shadow / refraction + reflection queries.  n <= 40. */
+ * shadow / refraction + reflection queries, [39] trace steps whose wave searched
+ * primary and other rays together.  n <= 40. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

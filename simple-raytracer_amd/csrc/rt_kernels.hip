@@ -165,6 +165,7 @@ struct Params {
     int lights_lds;                      // the lights' copy in LDS: float4 offset in rt_lds
     int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
     unsigned chunk;                      // work items a wave takes from the counter at a time (0: its idle lanes' count)
+    unsigned refill_min;                 // refill only when at least this many lanes are idle (or all are)
     void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
     int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
 };
@@ -188,7 +189,6 @@ constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading
 constexpr int kSpill = 8;
 static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack - 3 > kSpill, "stack spill blocks");
 constexpr int kBlock = 256;
-constexpr unsigned kChunkDefault = 64;   // work items a wave takes at a time: one 8x8 tile (pixel_xy)
 
 // ---------------------------------------------------------------------------
 // One lane's ray query (a TraceRay call + the consumer loop that follows it)
@@ -1370,6 +1370,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     cnt.trips = 0;
     cnt.trips_kind[0] = cnt.trips_kind[1] = cnt.trips_kind[2] = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
+    unsigned long long pc_mixed = 0;     // trace steps with primary and secondary/shadow searches together
     unsigned long long t_drain = 0;
 #endif
     for (;;) {
@@ -1389,19 +1390,25 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 busy = false;
             }
         }
-        // refill idle lanes: ballot + one atomic per wave + mbcnt prefix
+        // refill idle lanes: ballot + one atomic per wave + mbcnt prefix.
+        // Only once at least p.refill_min lanes are idle (or all are): the
+        // lanes a wave refills together start their pixels in the same phase
+        // and stay in step, so a trace step seldom mixes primary searches
+        // with the shorter shadow searches of other lanes, and the step,
+        // which lasts as long as its longest search, is not stretched by a
+        // few new primaries.  Idle lanes sit out the steps until then
+        // (C3 +10 %, C4 +30 %, C5 +50 % against refilling every idle lane at
+        // once; see refill_for).
         if (!drained) {
             unsigned long long idle = __ballot(!busy);
-            if (idle) {
+            if (idle && ((unsigned)__popcll(idle) >= p.refill_min || idle == ~0ull)) {
                 unsigned n = (unsigned)__popcll(idle);
                 int leader = __ffsll((long long)idle) - 1;
-                // The wave takes p.chunk work items at a time (a whole 8x8
-                // tile, or just its idle lanes' count when p.chunk = 0: see
-                // chunk_for) and refills its lanes from them: with tiles a
-                // wave's lanes stay on neighbouring pixels, whose rays walk
-                // the same nodes (profiles/r02/ab_chunk.txt).  Ranks < split
-                // take the rest of the current chunk, the others the start of
-                // the next one.
+                // The wave takes max(p.chunk, n) work items at a time and
+                // refills its lanes from them (p.chunk = 0, the default: just
+                // its idle lanes' count; option chunk = 64 keeps a wave on one
+                // 8x8 tile, chunk_for).  Ranks < split take the rest of the
+                // current chunk, the others the start of the next one.
                 const unsigned left = chunk_end - chunk_pos;
                 const unsigned base = chunk_pos, split = min(n, left);
                 unsigned nbase = 0;
@@ -1506,6 +1513,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             cnt.trips_kind[kind == RK_PRIMARY ? 0 : kind == RK_SHADOW ? 1 : 2] += (unsigned)d;
             for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o));
             pc_wtrips += (unsigned long long)d;
+            pc_mixed += (__ballot(search && kind == RK_PRIMARY) != 0ull) && (__ballot(search && kind != RK_PRIMARY) != 0ull);
             unsigned long long c2 = __builtin_amdgcn_s_memtime();
             pc_trace += c2 - c1;
 #endif
@@ -1547,6 +1555,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[12], pc_iter);
         atomicAdd(&st[13], pc_lanes);
         atomicAdd(&st[14], pc_wtrips);
+        atomicAdd(&st[39], pc_mixed);
     }
     atomicAdd(&st[15], (unsigned long long)cnt.trips);
     atomicAdd(&st[36], (unsigned long long)cnt.trips_kind[0]);
@@ -1620,7 +1629,8 @@ struct rt_scene {
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
-    long long opt_chunk = -1;          // refill chunk (-1: by the scene, chunk_for)
+    long long opt_chunk = -1;          // refill chunk (-1: default, chunk_for)
+    long long opt_refill_min = -1;     // idle lanes before a refill (-1: by the scene, refill_for)
     bool secondary = false;            // some material reflects (ks > 0) or refracts (opacity < 1, eta > 0)
     long long opt_reserve = 0;         // occupancy-derived grid: block slots left free for other kernels
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
@@ -1689,15 +1699,24 @@ size_t mode_lds_bytes(const rt_scene *s, int mode) {
     return mode_region_end(s, mode) + (size_t)s->base.nl * sizeof(LightK);
 }
 
-// Work items a wave takes from the pixel counter at a time.  A whole 8x8 tile
-// (kChunkDefault) when pixels spawn reflection / refraction rays: the wave's
-// secondary rays then leave neighbouring points of the same surfaces (C3 +5 %,
-// C3G +4.5 %, C5 +9 % against 0).  With primary and shadow rays only, a wave
-// takes exactly its idle lanes' count: tiles measured C4 -16 %, C2 -6 %
-// (profiles/r02/ab_chunk_auto.txt).  The image does not depend on it.
-static unsigned chunk_for(const rt_scene *s, const Params &p) {
-    if (s->opt_chunk >= 0) return (unsigned)s->opt_chunk;
-    return s->secondary && p.depth > 0 ? kChunkDefault : 0u;
+// Work items a wave takes from the pixel counter at a time: by default
+// exactly its idle lanes' count.  A whole 8x8 tile per wave (64) was +5 % on
+// C3 while every idle lane was refilled at once; with the deferred refill
+// (refill_for) it is -3 % on C3 and -10 % on C4, and it never changes the
+// image (profiles/r02/ab_chunk_auto.txt, ab_refill_min.txt).
+static unsigned chunk_for(const rt_scene *s) {
+    return s->opt_chunk >= 0 ? (unsigned)s->opt_chunk : 0u;
+}
+
+// How many lanes of a wave must be idle before it refills them.  With only
+// primary and shadow rays, a pixel lasts a few trace steps: the whole wave
+// starts 64 pixels together and finishes them before the next batch (C4
+// 10.9 G rays/s against 10.7 at 48 and 8.3 at 1).  With reflection /
+// refraction, 40 (C3 flat over 28..40, C5 flat over 40..56, C3D/C3G within
+// 2 % of their best; profiles/r02/ab_refill_min.txt).
+static unsigned refill_for(const rt_scene *s, const Params &p) {
+    if (s->opt_refill_min > 0) return (unsigned)s->opt_refill_min;
+    return s->secondary && p.depth > 0 ? 40u : 64u;
 }
 
 template <int MAXF, int MODE>
@@ -1711,7 +1730,8 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, hipStream_
     if (grid > need) grid = need;
     if (grid < 1) grid = 1;
     Params pl = p;
-    pl.chunk = chunk_for(s, p);
+    pl.chunk = chunk_for(s);
+    pl.refill_min = refill_for(s, pl);
     pl.lights_lds = (int)(mode_region_end(s, MODE) / sizeof(float4));
     const size_t cold_bytes = (size_t)grid * kBlock * MAXF * sizeof(Cold<MAXF>);
     size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
@@ -2288,7 +2308,8 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.dir_bf = 0;                      // set with the BVH (build_bvh); the scan needs none
     p.shadow_early_out = nan_fac ? 0 : 1;
     p.stack_cap = kLdsStackDefault;
-    p.chunk = kChunkDefault;           // launch_one: chunk_for
+    p.chunk = 0;                       // launch_one: chunk_for, refill_for
+    p.refill_min = 1;
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
     *out = s;
     return RT_OK;
@@ -2322,6 +2343,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "accel") s->opt_accel = value;
     else if (k == "inflight") return set_inflight(s, value);
     else if (k == "fail_bvh_upload") s->opt_fail_bvh_upload = value;
+    else if (k == "refill_min") {
+        if (value < 1 || value > 64) return RT_E_INVALID;
+        s->opt_refill_min = value;
+    }
     else if (k == "chunk") {
         if (value < 0 || value > 4096) return RT_E_INVALID;
         s->opt_chunk = value;

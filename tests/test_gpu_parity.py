@@ -511,21 +511,29 @@ def test_lds_stack_spill():
             gs.set_option("lds_stack", 11)
 
 
-def test_refill_chunk_bit_identical():
-    """How many work items a wave takes from the pixel counter at a time
-    (option chunk; by default a whole 8x8 tile when the scene spawns
-    reflection/refraction rays, else the idle lanes' count) decides which lane
-    renders which pixel, never a pixel's value: every chunk, including ones
-    that do not align with the 8x8 tiles and a ragged 37x23 image, gives the
-    same image and ray counts bit for bit."""
+def test_refill_options_bit_identical():
+    """How a wave refills its idle lanes decides which lane renders which
+    pixel and when, never a pixel's value.  Option chunk (work items taken
+    from the pixel counter at a time; default 0 = the idle lanes' count) and
+    option refill_min (idle lanes before a refill; default 40 when the scene
+    reflects or refracts, else 64), including chunks that do not align with
+    the 8x8 tiles and a ragged 37x23 image: the same image and ray counts bit
+    for bit, equal to the oracle's."""
+    variants = [{"chunk": c} for c in (1, 16, 64, 100, 256)]
+    variants += [{"refill_min": r} for r in (1, 7, 33, 64)]
+    variants += [{"chunk": 64, "refill_min": 1}, {"chunk": 100, "refill_min": 48}]
     for name, size in (("C3_64x64.txt", None), ("C4_32x32.txt", None), ("test7_s.txt", (37, 23))):
         ref, st = rtamd.render_scene(name, cwd=SCENES, imsize=size)
-        for c in (0, 1, 16, 64, 100, 256):
-            img, st2 = rtamd.render_scene(name, cwd=SCENES, imsize=size, options={"chunk": c})
-            assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, c)
-            assert _counts(st2) == _counts(st), (name, c)
-    with pytest.raises(rtamd.RTError):
-        rtamd.render_scene("test7_s.txt", cwd=SCENES, options={"chunk": -1})
+        o, o_cnt = OracleScene(name, cwd=SCENES).render(*(size or ()))
+        assert_parity(ref, o, f"{name} default refill")
+        assert _counts(st) == o_cnt
+        for opts in variants:
+            img, st2 = rtamd.render_scene(name, cwd=SCENES, imsize=size, options=opts)
+            assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, opts)
+            assert _counts(st2) == _counts(st), (name, opts)
+    for bad in ({"chunk": -1}, {"refill_min": 0}, {"refill_min": 65}):
+        with pytest.raises(rtamd.RTError):
+            rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
 
 @pytest.mark.parametrize("opts", [{"bvh_collapse": 0}, {"bvh_collapse": 1, "bvh_node": 1000}])

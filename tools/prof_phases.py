@@ -75,6 +75,7 @@ def main():
         "inner_trip_cycles": ({"fetch": c[30] / max(1, c[6] // 4), "trip": c[31] / max(1, c[6] // 4)}
                               if c[31] else None),
         "lane_trips_by_kind": dict(zip(["primary", "shadow", "refr_refl"], c[36:39])),
+        "mixed_step_frac": c[39] / iters if iters else None,   # steps with primary and other searches together
         "raw": c,
     }
     print(json.dumps(res, indent=1))
