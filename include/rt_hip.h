@@ -199,6 +199,11 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * "chunk" (0..4096: pixels a wave takes from the work counter at a time,
  * 0 = as many as it has idle lanes; default: 64, one 8x8 tile, when some
  * material reflects or refracts, else 0 -- never changes the image),
+ * "refill_min" (1..64: idle lanes a wave gathers before it refills them;
+ * default 40 when some material reflects or refracts, else 64), "gate_x"
+ * (0..64, default 32: reflection / refraction searches wait until that many
+ * lanes of the wave have one, unless nothing else would search) -- neither
+ * changes the image,
  * "fail_bvh_upload" (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 

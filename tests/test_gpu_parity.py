@@ -512,8 +512,10 @@ def test_lds_stack_spill():
 
 
 def test_refill_options_bit_identical():
-    """How a wave refills its idle lanes decides which lane renders which
-    pixel and when, never a pixel's value.  Option chunk (work items taken
+    """How a wave refills its idle lanes, and when it lets reflection /
+    refraction searches run (option gate_x: held back until that many lanes
+    have one), decide which lane renders which pixel and when, never a
+    pixel's value.  Option chunk (work items taken
     from the pixel counter at a time; default 0 = the idle lanes' count) and
     option refill_min (idle lanes before a refill; default 40 when the scene
     reflects or refracts, else 64), including chunks that do not align with
@@ -522,6 +524,7 @@ def test_refill_options_bit_identical():
     variants = [{"chunk": c} for c in (1, 16, 64, 100, 256)]
     variants += [{"refill_min": r} for r in (1, 7, 33, 64)]
     variants += [{"chunk": 64, "refill_min": 1}, {"chunk": 100, "refill_min": 48}]
+    variants += [{"gate_x": g} for g in (0, 1, 17, 64)] + [{"gate_x": 0, "refill_min": 1}]
     for name, size in (("C3_64x64.txt", None), ("C4_32x32.txt", None), ("test7_s.txt", (37, 23))):
         ref, st = rtamd.render_scene(name, cwd=SCENES, imsize=size)
         o, o_cnt = OracleScene(name, cwd=SCENES).render(*(size or ()))
@@ -531,7 +534,7 @@ def test_refill_options_bit_identical():
             img, st2 = rtamd.render_scene(name, cwd=SCENES, imsize=size, options=opts)
             assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, opts)
             assert _counts(st2) == _counts(st), (name, opts)
-    for bad in ({"chunk": -1}, {"refill_min": 0}, {"refill_min": 65}):
+    for bad in ({"chunk": -1}, {"refill_min": 0}, {"refill_min": 65}, {"gate_x": 65}):
         with pytest.raises(rtamd.RTError):
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
