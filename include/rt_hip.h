@@ -200,7 +200,8 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * 0 = as many as it has idle lanes; default: 64, one 8x8 tile, when some
  * material reflects or refracts, else 0 -- never changes the image),
  * "refill_min" (1..64: idle lanes a wave gathers before it refills them;
- * default 40 when some material reflects or refracts, else 64), "gate_x"
+ * default 32 when some material reflects or refracts, 48 above depth 4,
+ * 64 with primary and shadow rays only), "gate_x"
  * (0..64, default 32: reflection / refraction searches wait until that many
  * lanes of the wave have one, unless nothing else would search) -- neither
  * changes the image,

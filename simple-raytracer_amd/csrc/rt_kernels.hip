@@ -1732,11 +1732,13 @@ static unsigned chunk_for(const rt_scene *s) {
 // primary and shadow rays, a pixel lasts a few trace steps: the whole wave
 // starts 64 pixels together and finishes them before the next batch (C4
 // 10.9 G rays/s against 10.7 at 48 and 8.3 at 1).  With reflection /
-// refraction, 40 (C3 flat over 28..40, C5 flat over 40..56, C3D/C3G within
-// 2 % of their best; profiles/r02/ab_refill_min.txt).
+// refraction, 32 up to depth 4 (C3 +0.8 % over 40 in 4 rounds, C3G +0.9 %,
+// C3D -0.2 %) and 48 for deeper shade trees, whose pixels live longer (C5
+// +0.8 % over 40, -1.6 % at 32; profiles/r02/ab_refill_min.txt, ab_gate.txt).
 static unsigned refill_for(const rt_scene *s, const Params &p) {
     if (s->opt_refill_min > 0) return (unsigned)s->opt_refill_min;
-    return s->secondary && p.depth > 0 ? 40u : 64u;
+    if (!s->secondary || p.depth <= 0) return 64u;
+    return p.depth > 4 ? 48u : 32u;
 }
 
 template <int MAXF, int MODE>

@@ -517,7 +517,7 @@ def test_refill_options_bit_identical():
     have one), decide which lane renders which pixel and when, never a
     pixel's value.  Option chunk (work items taken
     from the pixel counter at a time; default 0 = the idle lanes' count) and
-    option refill_min (idle lanes before a refill; default 40 when the scene
+    option refill_min (idle lanes before a refill; default 32 or 48 when the scene
     reflects or refracts, else 64), including chunks that do not align with
     the 8x8 tiles and a ragged 37x23 image: the same image and ray counts bit
     for bit, equal to the oracle's."""
