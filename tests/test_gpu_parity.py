@@ -539,6 +539,22 @@ def test_refill_options_bit_identical():
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
 
+@pytest.mark.parametrize("opts", [{"gate_x": 64, "refill_min": 64}, {"gate_x": 64, "refill_min": 1}, {"gate_x": 0, "refill_min": 64}])
+def test_extreme_batching_deep_scene(opts):
+    """The batching options at their extremes on a depth-8 C5 miniature (long
+    shade trees: up to 8 levels of reflection / refraction per pixel): a wave
+    that holds every reflection / refraction search until all 64 lanes have
+    one, or refills only when all 64 lanes are idle, still drains (a held
+    search is released when nothing else would search) and renders the
+    oracle's image with its ray counts."""
+    img, st = rtamd.render_scene("C5_8x8.txt", cwd=SCENES, depth=8, options=opts)
+    o = OracleScene("C5_8x8.txt", cwd=SCENES)
+    o.set_depth(8)
+    ref, cnt = o.render()
+    assert_parity(img, ref, f"C5_8x8 depth 8 {opts}")
+    assert _counts(st) == cnt
+
+
 @pytest.mark.parametrize("opts", [{"bvh_collapse": 0}, {"bvh_collapse": 1, "bvh_node": 1000}])
 def test_bvh_collapse_parity(opts):
     """The 4-wide tree comes from the binary SAH tree by an SAH-optimal
