@@ -363,6 +363,11 @@ typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plan
 // 6 -> 5924, 12 -> 5849; with one leaf per round: 0 -> 5885, 2 -> 6021,
 // 5 -> 6031; profiles/r02/ab_leaf_*.txt)
 constexpr unsigned kLeafWait = 2;
+// The depth > 4 instantiation (MAXF 9/17: C5, depth 8, whose 100 000-sphere
+// tree is 12 levels deep) keeps descending until 12 lanes lack a leaf: C5
+// +2.2 % (2: C3 best, 8 there -1.2 %; a run-time threshold cost C3 1 %,
+// profiles/r02/ab_leafwait_r2final.txt)
+constexpr unsigned leaf_wait_for(int maxf) { return maxf > 5 ? 12u : kLeafWait; }
 constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
 constexpr int kNStats = 40;                      // device counter slots (rt_scene_debug_counters)
 
@@ -508,7 +513,7 @@ __device__ __forceinline__ float child_entry(const ChildPlanes &cp, int i, float
 // the plane distances are the child boxes' offsets from po, and a cone test
 // per child instead of the slab test; its leaves are still tested with the
 // query's own ray (q.o, q.d).
-template <bool point>
+template <bool point, unsigned LEAF_WAIT = kLeafWait>
 __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, int root = 0,
                           V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
     // |1/d| capped at 2^100 (1/0 -> 1e30 as before): the quantised planes'
@@ -666,7 +671,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
 #endif
             // all but kLeafWait lanes hold a leaf: visit the leaves now (the
             // few still descending wait one leaf round)
-            if ((unsigned)__popcll(__ballot(leaf == rtbvh::kEmpty)) <= kLeafWait) break;
+            if ((unsigned)__popcll(__ballot(leaf == rtbvh::kEmpty)) <= LEAF_WAIT) break;
         }
         // visit the parked leaf; a leaf the lane stopped on is parked for the
         // next round (one leaf per lane per round: +0.8 % over visiting them
@@ -1505,7 +1510,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(search && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (search && !q.bf) bvh_trace<false>(q, p, stk, cnt);
+            if (search && !q.bf) bvh_trace<false, leaf_wait_for(MAXF)>(q, p, stk, cnt);
             if (skip) {
                 q.closest = true;
                 q.unb = false;
