@@ -1302,26 +1302,20 @@ __device__ __forceinline__ int image_row(const Params &p, int r) {
     return p.y0 + (r / p.rblock) * p.rstep + r % p.rblock;
 }
 
-// Pixel index -> (x, y): strips of 8 rows, 8x8 tiles along the strip, so a
-// wave's 64-index chunk is one tile. Inside a whole tile the indices run in Z
-// order, so the few lanes a wave refills at once get a compact 2x2 / 4x4 group
-// (+0.6 % on C3, every A/B round); a partial tile (W % 8, the last strip) keeps
-// column order. Both are bijections, so the image does not change.
-
+// Pixel index -> (x, y): strips of kStrip rows, column by column along the
+// strip, so a refill batch of consecutive indices is a compact block of
+// pixels (32 lanes: 4 columns x 8 rows).  Z order inside 8x8 tiles was +0.6 %
+// while every idle lane was refilled at once; with the batched refill column
+// order is C3 +1.9 %, C5 +2.5 % (profiles/r02/ab_pixel_order.txt).  A
+// bijection, so the image does not change.
+constexpr int kStrip = 8;   // 4 / 16-row strips: C3 -1.6 / -4 %, C5 -3.7 / -3.9 %
 __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, int &y) {
-    unsigned strip_px = (unsigned)p.W * 8u;
+    unsigned strip_px = (unsigned)p.W * (unsigned)kStrip;
     unsigned s = idx / strip_px;
     unsigned r = idx - s * strip_px;
-    int sh = min(8, p.rows - (int)s * 8);
-    const unsigned t = r >> 6;
-    if (sh == 8 && (int)(t * 8 + 8) <= p.W) {      // a whole 8x8 tile: Z order inside it
-        const unsigned rr = r & 63u;
-        x = (int)(t * 8 + ((rr & 1u) | ((rr >> 1) & 2u) | ((rr >> 2) & 4u)));
-        y = (int)s * 8 + (int)(((rr >> 1) & 1u) | ((rr >> 2) & 2u) | ((rr >> 3) & 4u));
-        return;
-    }
+    int sh = min(kStrip, p.rows - (int)s * kStrip);
     x = (int)(r / (unsigned)sh);
-    y = (int)s * 8 + (int)(r % (unsigned)sh);
+    y = (int)s * kStrip + (int)(r % (unsigned)sh);
 }
 
 // Primary ray of local pixel (x, y): p = ul + dh * x + dv * row, direction
