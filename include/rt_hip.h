@@ -173,6 +173,16 @@ int rt_scene_prepare(rt_scene *scene, const rt_camera *cam, int W, int H);
 int rt_render_row_blocks(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int block, int step,
                          int nrows, float *out_rgb, rt_stats *stats);
 
+/* Render a list of n pixels of the W x H image: xy holds n (x, y) pairs
+ * (host memory), out_rgb receives n * 3 floats (host memory), pixel k's
+ * colour at out_rgb[3k..3k+2] -- bit for bit the colour the whole-image
+ * render gives that pixel; stats count the list's rays only.  Synchronous,
+ * on the scene's stream after every render issued before.  (Sparse
+ * re-renders; the parity tests use it for exact per-pixel ray counts on
+ * samples of full-size images.)  stats may be NULL. */
+int rt_render_pixels(rt_scene *scene, const rt_camera *cam, int W, int H, const int *xy, int n, float *out_rgb,
+                     rt_stats *stats);
+
 /* Put gathered row sets back in image order, on the device (the multi-device
  * CLI: after an RCCL gather of every device's rt_render_row_blocks buffer).
  * gathered holds `world` buffers of rows_per * W * 3 floats, buffer r being

@@ -1,76 +1,3 @@
-# Integrating the MI355X hot path into the reference
-
-The reference (zachoines/simple-raytracer) is one C++20 program. Its hot path is
-the call at `main.cpp:607`:
-
-```cpp
-Mat3D matt = create_view_window_and_ray_trace(view_origin, view_direction.norm(),
-                                              view_up.norm(), fov_h, height, width,
-                                              background_color);
-```
-
-`create_view_window_and_ray_trace` (`main.cpp:670-767`) runs the pixel loop. It calls
-`TraceRay` (`main.cpp:1215-1407`) and `ShadeRay` (`main.cpp:783-1207`) and reads the
-scene from the global `Globals environment` (`main.cpp:58`). This repo replaces that
-call with the C ABI in `include/rt_hip.h` (GPU layer, `librt_hip.so`). The ABI has no
-C++ types, no exceptions and no torch types.
-
-There are two ways to adopt it.
-
-## 1. Drop-in executable (no reference changes)
-
-`simple-raytracer_amd/lib/rt` is a replacement for the `SimpleRayTracer` binary:
-
-```
-rt scene.txt                 # writes scene.ppm in the reference's P3 format
-rt scene.txt --gpus 8        # 8-row blocks dealt round robin to 8 devices of one node,
-                             # each device copies its rows to the host
-rt scene.txt --gpus 8 --gather rccl   # same rows gathered with RCCL (ncclGather to the
-                             # first device over xGMI, device-side de-interleave, one
-                             # copy to the host); opt-in until a multi-device node has
-                             # run test_cli_rccl_gather_multi_device
-rt scene.txt --depth 8 --imsize 16384 16384 --stats
-```
-
-It behaves like `main.cpp:60-657`:
-- it reads the same scene files and keyword quirks;
-- it prints the same stdout/stderr messages and uses the same exit behaviour;
-- it writes the same P3 output, including `"P3 \n"` and `18446744071562067968` for NaN.
-
-`tests/test_gpu_parity.py::test_cli_drop_in` compares the output PPM with the
-reference's on six scenes. Five are md5-identical. On `test7.txt` one 8-bit value of
-3 499 200 differs: its float is 9e-8 from a quantisation level boundary (every such
-value is checked to be one level off with a float within 1e-4 of the edge, and
-counted). `test_cli_rccl_gather` checks that `--gather rccl` and `--gather host` give
-the same bytes.
-
-## 2. Linking the GPU layer into the reference's own `main`
-
-A maintainer keeps the reference's parser and writer and swaps only the seam. The
-binding is `integration/rt_hip_binding.cpp` (listed in full below). It defines the
-reference's own `create_view_window_and_ray_trace` with the reference's own types
-(`src/definitions.h`, included in place), converts `environment` into an
-`rt_scene_desc` (textures `Mat3D` → bytes included), computes the view window exactly
-as `main.cpp:677-710` does with the reference's `Vector3` arithmetic, renders through
-`rt_render_rows`, and quantises into the reference's `Mat3D`.
-
-It is compiled and run, not just shown:
-- `tests/test_integration.py` compiles it with
-  `g++ -std=c++20 -fsyntax-only -Wall -Wextra -Werror -I/root/reference -Iinclude`
-  (skipped where the reference's sources are absent), and checks that the listing
-  below is the file;
-- `oracle/Makefile` target `ref-hip` links it with the reference's own `main.cpp`,
-  compiled from `/root/reference` with `-fPIC` (the call at `main.cpp:607` then goes
-  through the symbol) and its definition of the seam made weak with
-  `objcopy --weaken-symbol`, into `oracle/_ref/SimpleRayTracer_hip`;
-- `tests/test_gpu_parity.py::test_reference_main_with_hip_seam` runs that binary on
-  six example scenes and compares its PPMs with the reference's (md5, or counted
-  rounding flips, as for the drop-in CLI).
-
-For a maintainer the change is: add the file, delete `main.cpp:670-767`, and link
-`-I<repo>/include -L<repo>/simple-raytracer_amd/lib -lrt_hip -lrt_host`.
-
-```cpp
 // rt_hip_binding.cpp -- the reference-side binding: what a maintainer of
 // zachoines/simple-raytracer adds to route its hot path through this repo's
 // C ABI (include/rt_hip.h, librt_hip.so).
@@ -247,47 +174,3 @@ Mat3D create_view_window_and_ray_trace(Vector3 view_origin, Vector3 view_directi
             for (int c = 0; c < 3; c++) matt(i, j, c) = (size_t)q[((size_t)i * W + j) * 3 + c];
     return matt;
 }
-```
-
-### Entry points and the reference interface each one replaces
-
-| C ABI (`include/rt_hip.h`) | Replaces |
-|---|---|
-| `rt_scene_create(dev, desc, &scene)` | the implicit reads of `environment` (`main.cpp:58`, `src/definitions.h:304-311`) by `TraceRay`/`ShadeRay`; uploads the scene to device `dev` |
-| `rt_render_rows(scene, cam, W, H, y0, y1, out, stats)` | `create_view_window_and_ray_trace` (`main.cpp:670-767`) for rows `[y0, y1)`, which includes every `TraceRay` (`:1215`) and `ShadeRay` (`:783`) call under it; returns pre-quantisation float RGB |
-| `rt_render_rows_async(..., hip_stream)` + `rt_scene_last_stats` | same, asynchronous on a caller stream (multi-GPU / benchmarking) |
-| `rt_render_row_blocks(...)` / `rt_render_row_blocks_async(..., y0, block, step, nrows, ...)` | the pixel loop over a block-interleaved row set (rank r of N: `y0 = 8r`, `block = 8`, `step = 8N`), the multi-GPU partition |
-| `rt_scene_set_option(scene, "inflight", n)` | — (new): n renders of the scene may run at once (independent frames on different caller streams overlap; one frame's tail is filled by the next) |
-| `rt_render_pixels(scene, cam, W, H, xy, n, out, stats)` | — (new): the colours of a list of pixels, bit for bit the whole-image render's, with the list's own ray counts (sparse re-renders; the parity tests' exact per-pixel counts on full-size samples) |
-| `rt_deinterleave_rows(gathered, world, rows_per, W, H, block, image, stream)` | — (new): the multi-device CLI's device-side reassembly after its RCCL gather (the reference's one image `Mat3D`, `main.cpp:717`) |
-| `rt_scene_prepare(scene, cam, W, H)` | — (new, optional): BVH for the camera and the render slots' buffers up front, so no render pays for them |
-| `rt_scene_destroy` | — (the reference never frees its scene) |
-| `rt_device_count`, `rt_strerror`, `rt_scene_set_option` | — (new) |
-
-| C ABI (`include/rt_host.h`) | Replaces |
-|---|---|
-| `rth_parse_file` | the parser `main.cpp:88-602` (keywords `src/config.h:17-50`) and `read_texture` (`src/utility.h:59-139`) |
-| `rth_camera` | `main.cpp:677-710` |
-| `rth_quantize` | `main.cpp:760-762` (x86 `cvttss2si` semantics: NaN → `INT_MIN`) |
-| `rth_write_ppm`, `rth_output_path` | `main.cpp:613-650`, `remove_extension` (`src/utility.h:34-41`) |
-| `rth_row_set(H, world, rank, block, ...)` | the row loop `main.cpp:718` dealt to `world` devices (the CLI's and the bench's partition) |
-
-### Errors
-
-Every function returns `RT_OK` (0) or a negative `RT_E_*` code. `rt_strerror` gives the
-text. Nothing throws across the ABI. `rth_parse_file` returns:
-- `> 0` where the reference prints a message and exits 0;
-- `< 0` where the reference throws. The message then holds the `std::cerr` lines it
-  prints, and the CLI rethrows the same exception type.
-
-### Python
-
-`simple-raytracer_amd/rtamd/__init__.py` is the ctypes binding used by the tests and
-`bench.py`:
-
-```python
-import sys; sys.path.insert(0, "simple-raytracer_amd")
-import rtamd
-img, stats = rtamd.render_scene("scene.txt")   # float32 HxWx3 + ray counters
-rtamd.write_ppm("scene.ppm", img)
-```

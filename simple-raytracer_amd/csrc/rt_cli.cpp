@@ -8,10 +8,12 @@
 //   bad command          -> std::cerr lines, uncaught exception (abort)
 // New optional flags (the reference has none): --depth N, --imsize W H,
 // --gpus N (rows dealt to N devices in 8-row blocks), --device D,
-// --gather rccl|host (how the devices' rows come together; default rccl for
-// N > 1: one RCCL gather to the first device over xGMI, a device-side
-// de-interleave and one copy to the host; host: each device copies its rows
-// to the host), --float-out FILE (raw float32 H*W*3 framebuffer), --stats.
+// --gather host|rccl (how the devices' rows come together; host, the default:
+// each device copies its rows to the host; rccl: one RCCL gather to the first
+// device over xGMI, a device-side de-interleave and one copy to the host --
+// opt-in until a multi-device node has run tests/test_gpu_parity.py::
+// test_cli_rccl_gather_multi_device), --float-out FILE (raw float32 H*W*3
+// framebuffer), --stats.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -172,7 +174,7 @@ int main(int argc, char *argv[]) {
     }
     if (gpus < 1) gpus = 1;
     if (gpus > ndev - device) gpus = ndev - device;
-    if (gather.empty()) gather = gpus > 1 ? "rccl" : "host";
+    if (gather.empty()) gather = "host";
     if (gather != "rccl" && gather != "host") {
         std::cerr << "rt: --gather must be rccl or host" << std::endl;
         return 2;

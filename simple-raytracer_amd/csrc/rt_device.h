@@ -1,0 +1,171 @@
+// rt_device.h -- what the render kernel (rt_kernels.hip) and the host side
+// (rt_scene.cpp: scene upload, render slots, the rt_hip.h C ABI) share: the
+// float semantics of the reference's Vector3 / Color (src/definitions.h:18-195),
+// the device scene layout (Params and its arrays), and the
+// launch interface of the kernels.  Internal to librt_hip.so.
+#ifndef RT_DEVICE_H
+#define RT_DEVICE_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace rt {
+
+// ---------------------------------------------------------------------------
+// Device-side geometry/colour semantics of src/definitions.h
+// ---------------------------------------------------------------------------
+struct V3 {
+    float x, y, z;
+};
+struct C3 {
+    float r, g, b;
+};
+
+__host__ __device__ __forceinline__ V3 vadd(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__host__ __device__ __forceinline__ V3 vsub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__host__ __device__ __forceinline__ V3 vmul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__host__ __device__ __forceinline__ V3 vdiv(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__host__ __device__ __forceinline__ float vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ V3 vnorm(V3 a) { return vdiv(a, sqrtf(vdot(a, a))); }
+__host__ __device__ __forceinline__ V3 vcross(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+// std::clamp(v, 0, 1): NaN passes through (not fminf/fmaxf)
+__device__ __forceinline__ float clamp01(float v) { return (v < 0.0f) ? 0.0f : ((1.0f < v) ? 1.0f : v); }
+__device__ __forceinline__ float clampr(float v, float lo, float hi) { return (v < lo) ? lo : ((hi < v) ? hi : v); }
+__device__ __forceinline__ C3 cmulc(C3 a, C3 b) { return {clamp01(b.r * a.r), clamp01(b.g * a.g), clamp01(b.b * a.b)}; }
+__device__ __forceinline__ C3 cmulf(C3 a, float f) { return {clamp01(f * a.r), clamp01(f * a.g), clamp01(f * a.b)}; }
+__device__ __forceinline__ C3 cadd(C3 a, C3 b) { return {clamp01(b.r + a.r), clamp01(b.g + a.g), clamp01(b.b + a.b)}; }
+__device__ __forceinline__ float max0(float x) { return (0.0f < x) ? x : 0.0f; }
+
+constexpr double kPi = 3.14159265358979323846;        // src/config.h:11
+constexpr double kRightAngle = 90.0 * kPi / 180.0;    // main.cpp:964
+constexpr float kFltMax = 3.40282347e+38f;            // std::numeric_limits<float>::max()
+
+enum { ENTERING = 0, EXITING = 1 };
+
+// ---------------------------------------------------------------------------
+// Device scene layout (built by rt_scene_create)
+// ---------------------------------------------------------------------------
+// Faces (object index 0..nf-1), 5 x float4 each, per-face invariants hoisted
+// exactly as TraceRay computes them (main.cpp:1280-1301, :1361-1366):
+//   [0] v0.xyz, D = -n.v0     [1] n.xyz, det = d11*d22 - d12*d12
+//   [2] e1.xyz, d11           [3] e2.xyz, d22        [4] d12, -, -, -
+// Spheres (object index nf..nf+ns-1): float4 center.xyz, radius.
+struct ObjK {                 // per object, shading data
+    float dif[3], ka;
+    float spc[3], kd;
+    float ks, n, opacity, eta;
+    int tex;                  // texture index or -1
+    int is_sphere;
+    int pad[2];
+};
+struct FaceShadeK {           // per face, shading-only data
+    float vn[3][3];           // vertex_normal[k].norm() (main.cpp:1382-1384)
+    float vt[3][2];           // clamp<float>(texture_coords, 0, 1) (main.cpp:835-841)
+    int smooth;
+    int pad[2];
+};
+struct LightK {
+    float xyz[3], w;          // position or direction, w
+    float col[3], pad0;
+    float L[3], pad1;         // directional: light.direction.norm() * -1 (main.cpp:887)
+    float sdir[3], pad2;      // directional: light.direction * -1 (main.cpp:895, unnormalised)
+};
+static_assert(sizeof(LightK) % sizeof(float4) == 0, "lights are staged in LDS as float4s");
+struct TexK {
+    int w, h;
+    long long off;                       // first byte in Params::texels
+};
+// directional light: its shadow-region tree over the spheres (rt host:
+// dir_trees) -- root node in Params::bvh (-1: no sphere can shadow) and the
+// rotation R (rows) into the frame the tree's boxes were built in
+struct DirK {
+    float R[9];
+    int root;
+    float cone_k;                        // max(0, |d|^2 - 1), rounded up
+    float cone_h;                        // |d| < 1: height bound of the shadow region, else +inf
+};
+
+struct Params {
+    const float4 *__restrict__ fscan;
+    const float4 *__restrict__ sscan;
+    const float *__restrict__ ofac;      // (float)(1.0 - opacity) per object (main.cpp:909)
+    const ObjK *__restrict__ objs;
+    const FaceShadeK *__restrict__ fsh;
+    const LightK *__restrict__ lights;
+    const unsigned char *__restrict__ texels;   // all textures: RGB bytes, row-major
+    const TexK *__restrict__ texs;
+    float *__restrict__ out;
+    unsigned int *__restrict__ work;     // pixel work counter
+    unsigned long long *__restrict__ stats;
+    int nf, ns, nl;
+    float bkg[3];
+    float eta_bkg, eps;
+    int depth;
+    float eye[3], ul[3], dh[3], dv[3];
+    int W, y0, rows;                     // render `rows` rows of a W-wide image: local row r is
+    int rblock, rstep;                   // image row y0 + (r / rblock) * rstep + r % rblock
+    unsigned int total;                  // W * rows, or the pixel list's length
+    const int *__restrict__ pix;         // pixel list (x, y pairs; rt_render_pixels) or null: work item k
+                                         // is pixel (pix[2k], pix[2k+1]), its colour goes to out[3k..3k+2]
+    // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
+    const float4 *__restrict__ bvh;
+    const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
+    int dir_bf;                          // directional lights in a scene with spheres: 0 none,
+                                         // 1 brute-force scan, 2 faces by the BVH + shadow-region trees
+    const DirK *__restrict__ dirk;       // per light (dir_bf == 2)
+    int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
+    int ovf_stride;                      // BVH: stack spill entries per lane (deepest tree, kSpill multiple)
+    int lights_lds;                      // the lights' copy in LDS: float4 offset in rt_lds
+    int nl_lds;                          // lights [0, nl_lds) are in LDS, the rest read from `lights`
+    int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
+    unsigned chunk;                      // work items a wave takes from the counter at a time (0: its idle lanes' count)
+    unsigned refill_min;                 // refill only when at least this many lanes are idle (or all are)
+    unsigned gate_x;                     // hold reflection/refraction searches until this many lanes have one
+    void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
+    int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
+};
+
+enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
+#ifndef RT_PROF
+#define RT_PROF 0                        // 1: per-wave cycle/occupancy counters in stats[9..15]
+#endif
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
+#endif
+// Largest worst-case BVH stack a tree may need (entries per lane; the spill
+// area is sized per tree, Params::ovf_stride).  Refill tags kRefill + b stay
+// far below the leaf links (> INT_MIN + 256) for b <= kStackMax / kSpill.
+constexpr int kStackMax = 1024;
+// BVH traversal stack entries per lane in LDS (entry 0: the sentinel); a
+// deeper stack spills its oldest kSpill entries to device memory (rare)
+constexpr int kLdsStack = 16;            // most entries the LDS share may hold (option lds_stack)
+constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading state): 5 blocks per CU
+                                         // on paper, -8.6 % measured; 14: 270 spills per C3 frame
+constexpr int kSpill = 8;
+static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack - 3 > kSpill, "stack spill blocks");
+constexpr int kBlock = 256;
+constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
+constexpr int kNStats = 40;              // device counter slots (rt_scene_debug_counters)
+constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS (rt_kernels.hip LW_*)
+
+// ---------------------------------------------------------------------------
+// Launch interface (rt_kernels.hip)
+// ---------------------------------------------------------------------------
+// MAXF, the ShadeRay frames per lane an instantiation holds, for a recursion
+// depth: 5 (depth <= 4), 9 (<= 8), 17 (<= 16); -1 above
+int maxf_for_depth(int depth);
+// resident workgroups per CU of render_kernel<maxf, mode> with `lds_bytes` of
+// dynamic LDS (0 if it cannot launch)
+int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes);
+// bytes of one lane's cold ShadeRay frame (Cold<maxf>)
+size_t cold_frame_bytes(int maxf);
+hipError_t render_launch(int maxf, int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st);
+hipError_t deinterleave_launch(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
+                               hipStream_t st);
+
+}  // namespace rt
+
+#endif  // RT_DEVICE_H

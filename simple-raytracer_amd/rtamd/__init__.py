@@ -88,7 +88,7 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
                 "rth_output_path", "rth_row_set"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
-               "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks",
+               "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_deinterleave_rows", "rt_strerror"]
 
@@ -146,6 +146,9 @@ def hip_lib() -> C.CDLL:
                                                  C.c_void_p]
         L.rt_render_row_blocks.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                            C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(rt_stats)]
+        if hasattr(L, "rt_render_pixels"):   # absent from round-1/2 libraries (A/B baselines)
+            L.rt_render_pixels.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_void_p,
+                                           C.c_int, C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_prepare.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
@@ -316,6 +319,16 @@ class GpuScene:
         _check(hip_lib().rt_render_row_blocks(self._h, C.byref(cam), W, H, y0, block, step, nrows,
                                               C.c_void_p(out.ctypes.data), C.byref(st)),
                "rt_render_row_blocks")
+        return out, st
+
+    def render_pixels(self, cam: rt_camera, W: int, H: int, xy):
+        """rt_render_pixels: the colours of the listed (x, y) pixels of the
+        W x H image -> (float32 [n, 3], rt_stats of those pixels' rays)."""
+        xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
+        out = np.empty((len(xy), 3), dtype=np.float32)
+        st = rt_stats()
+        _check(hip_lib().rt_render_pixels(self._h, C.byref(cam), W, H, C.c_void_p(xy.ctypes.data), len(xy),
+                                          C.c_void_p(out.ctypes.data), C.byref(st)), "rt_render_pixels")
         return out, st
 
     def prepare(self, cam: rt_camera, W: int, H: int) -> None:

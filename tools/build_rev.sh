@@ -5,8 +5,12 @@ set -eu
 cd "$(dirname "$0")/.."
 rev=$1; var=$2; shift 2
 d=$(mktemp -d /tmp/rtrev.XXXXXX)
-git show "$rev:simple-raytracer_amd/csrc/rt_kernels.hip" > "$d/rt_kernels.hip"
-git show "$rev:simple-raytracer_amd/csrc/rt_bvh.h" > "$d/rt_bvh.h"
-make -C simple-raytracer_amd VARIANT="$var" KSRC="$d/rt_kernels.hip" EXTRA="${*:-}" -B -j8 >/dev/null
+git archive "$rev" simple-raytracer_amd/csrc include | tar -x -C "$d"
+if [ -f "$d/simple-raytracer_amd/csrc/rt_scene.cpp" ]; then
+  make -C simple-raytracer_amd VARIANT="$var" SRC="$d/simple-raytracer_amd/csrc" INC="$d/include" EXTRA="${*:-}" -B -j8 >/dev/null
+else   # before the host side moved out of rt_kernels.hip
+  make -C simple-raytracer_amd VARIANT="$var" SRC="$d/simple-raytracer_amd/csrc" KSRC="$d/simple-raytracer_amd/csrc/rt_kernels.hip" \
+       KDEPS="$d/simple-raytracer_amd/csrc/rt_kernels.hip" INC="$d/include" EXTRA="${*:-}" -B -j8 >/dev/null
+fi
 rm -rf "$d"
 echo "built simple-raytracer_amd/lib_$var from $rev"

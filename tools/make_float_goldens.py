@@ -47,14 +47,14 @@ MAX_PX = 256 * 256
 PRELUDE = r'''
 #include <cstdio>
 #include <cstdlib>
-static unsigned long long rt_cnt[4];   // primary, shadow, refraction, reflection
+static unsigned long long rt_cnt[5];   // primary, shadow, refraction, reflection, back() on an empty stack
 static FILE *rt_float_dump() {
     static FILE *f = std::getenv("RT_FLOAT_DUMP") ? std::fopen(std::getenv("RT_FLOAT_DUMP"), "wb") : nullptr;
     return f;
 }
 static void rt_write_counts() {
     if (FILE *f = std::getenv("RT_COUNT_DUMP") ? std::fopen(std::getenv("RT_COUNT_DUMP"), "w") : nullptr) {
-        std::fprintf(f, "%llu %llu %llu %llu\n", rt_cnt[0], rt_cnt[1], rt_cnt[2], rt_cnt[3]);
+        std::fprintf(f, "%llu %llu %llu %llu %llu\n", rt_cnt[0], rt_cnt[1], rt_cnt[2], rt_cnt[3], rt_cnt[4]);
         std::fclose(f);
     }
 }
@@ -78,6 +78,11 @@ PATCHES = [
      "        ++rt_cnt[2];\n"),
     ("        for (auto& [object, intersections] : TraceRay(incidence_object_intersection.point, R))",
      "        ++rt_cnt[3];\n"),
+    # main.cpp:1028: back() of the copied medium stack when it is empty (UB in
+    # the reference: the value it reads is not defined) -- counted, so that a
+    # fixture records whether any pixel went through it
+    ("                    new_incident_refraction_index = new_incident_object_stack.back()->material.refraction_index;",
+     "                    if (new_incident_object_stack.empty()) ++rt_cnt[4];\n"),
 ]
 
 
@@ -114,10 +119,15 @@ def run(exe: str, scene_path: str, cwd: str, depth: int | None, work: str):
         os.remove(tmp)
     f = np.fromfile(fd, dtype=np.float32).reshape(h, w, 3)
     c = [int(x) for x in open(cnt).read().split()]
-    return f, md5, dict(zip(("primary", "shadow", "refraction", "reflection"), c))
+    return f, md5, dict(zip(("primary", "shadow", "refraction", "reflection"), c[:4])), c[4]
 
 
 def main() -> None:
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None,
+                    help="(re)make just these fixtures and merge them into the existing index")
+    only = ap.parse_args().only
     gold = json.load(open(os.path.join(GOLD, "golden.json")))
     os.makedirs(OUT, exist_ok=True)
     work = tempfile.mkdtemp(prefix="rt_ref_instr_")
@@ -137,22 +147,33 @@ def main() -> None:
     # C3 variants with a directional light (unnormalised direction, spheres)
     # and with glass triangles (SKIP_TRANS), at 64x64
     gen_specs = {"C5_12x12@d8": ("C5", 12, 12)}
+    # C5 at its BASELINE depth 8 on a larger miniature (1024 pixels; the
+    # reference takes minutes on it: 100 000 spheres, brute force)
+    c5b = os.path.join(work, "C5_32x32.txt")
+    open(c5b, "w").write(gen.scene_text("C5", w=32, h=32))
+    jobs.append(("C5_32x32@d8", c5b, work, 8))
+    gen_specs["C5_32x32@d8"] = ("C5", 32, 32)
     for cfg in ("C3D", "C3G"):
         path = os.path.join(work, f"{cfg}_64x64.txt")
         open(path, "w").write(gen.scene_text(cfg, w=64, h=64))
         jobs.append((f"{cfg}_64x64", path, work, None))
         gen_specs[f"{cfg}_64x64"] = (cfg, 64, 64)
     index = {}
+    if only is not None:
+        with open(os.path.join(OUT, "index.json")) as fh:
+            index = json.load(fh)
+        jobs = [j for j in jobs if j[0] in only]
     for fix, scene, cwd, depth in jobs:
         path = scene if os.path.isabs(scene) else os.path.join(cwd, scene)
-        f, md5, cnt = run(exe, path, cwd, depth, work)
+        f, md5, cnt, ub = run(exe, path, cwd, depth, work)
         base = os.path.basename(scene)
         if depth is None and base in gold:
             assert md5 == gold[base]["md5"], f"{fix}: instrumented build changed the output"
             assert sum(cnt.values()) == gold[base]["trace_calls"], (fix, cnt)
         np.savez_compressed(os.path.join(OUT, fix + ".npz"), f=f)
         index[fix] = dict(scene=base, depth=4 if depth is None else depth, width=f.shape[1],
-                          height=f.shape[0], md5=md5, counts=cnt, nan_px=int(np.isnan(f).any(-1).sum()))
+                          height=f.shape[0], md5=md5, counts=cnt, nan_px=int(np.isnan(f).any(-1).sum()),
+                          ub_back=ub)
         if fix in gen_specs:
             c, w, h = gen_specs[fix]
             index[fix]["generated"] = {"config": c, "w": w, "h": h}
