@@ -34,8 +34,8 @@ FLOP_SPHERE, FLOP_TRI = 20, 42  # algorithmic FLOPs per ray-primitive test (SURV
 # ray-box test as the kernel executes it per child box: 6 plane
 # distances by FMA (12 FLOP), entry = max of 3 near distances and tmin (3),
 # exit = min of 3 far distances and tmax (3), entry <= exit (1) -- the octant
-# selects near/far planes without per-axis min/max; the 6 u8->f32 conversions
-# of the quantised bounds are not counted
+# selects near/far planes without per-axis min/max; the binary16 bounds are
+# converted inside the FMA (v_fma_mix_f32), so there is nothing else to count
 FLOP_BOX = 19
 
 WORKLOADS = {
@@ -98,7 +98,7 @@ def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
         t0 = time.perf_counter()
         subprocess.run([ref, os.path.basename(path)], cwd=d, check=True, stdout=subprocess.DEVNULL)
         dt = time.perf_counter() - t0
-        return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
+        return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference", "host": host_cores(),
                 "sample": f"{config} scene at {sample}x{sample} (full field of view), {rays} rays, "
                           f"{dt:.1f} s, single-threaded reference binary"}
     # fall back to this repo's C restatement on all cores (a port, not the reference)
@@ -126,14 +126,27 @@ def cpu_port_baseline(config: str, sample: int) -> dict:
     path = gen.write_scene(d, config, w=sample, h=sample, tag=f"{config}_{sample}_port")
     o = OracleScene(path)
     o.set_depth(gen.CONFIGS[config]["depth"])
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    host = host_cores()
+    threads = host["omp_num_threads"] or host["affinity"]
     t0 = time.perf_counter()
     _, cnt = o.render(threads=threads)
     dt = time.perf_counter() - t0
     r = sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection"))
-    return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port", "host": host,
             "sample": f"{config} scene at {sample}x{sample} (full field of view), {r} rays, {dt:.1f} s, "
-                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows"}
+                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows on {threads} threads"}
+
+
+def host_cores() -> dict:
+    """What the CPU legs may use: the machine's CPUs (nproc of the node), the
+    ones this process may run on (its affinity: a GPU lease's share), and
+    OMP_NUM_THREADS (0 when unset)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": aff,
+            "omp_num_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or 0)}
 
 
 def load_pmc_traffic(config: str):
@@ -266,6 +279,11 @@ def main() -> None:
 
     if rank == 0:
         value = rays_total * args.steps / elapsed / 1e6
+        # rays actually searched: shadow rays whose cumulative mask was already
+        # 0 are TraceRay calls of the reference (so in `value`) but are not
+        # searched (their result is known); rank 0's share scaled to the job
+        known = float(st.shadow_known) * (rays_total / my_rays if my_rays else 0.0)
+        value_traced = (rays_total - known) * args.steps / elapsed / 1e6
         ns, nt = cfg["spheres"], cfg["tris"]
         bf_flop_per_ray = FLOP_SPHERE * ns + FLOP_TRI * nt
         # dominant kernel = render_kernel; per launch on rank 0 (its strip).
@@ -298,6 +316,7 @@ def main() -> None:
             "metric": "Mrays/s (primary+secondary)",
             "value": round(value, 3),
             "unit": "Mrays/s",
+            "value_traced": round(value_traced, 3),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -317,14 +336,17 @@ def main() -> None:
                        "launch": {"blocks_per_cu": int(dbg[17]), "grid": int(dbg[18]),
                                   "lds_bytes_per_block": int(dbg[19]), "bvh_nodes": int(dbg[20])}},
             "one_frame": {"Mrays_per_s": round(my_rays / k_s / 1e6, 3) if world == 1 else None,
+                          "Mrays_per_s_traced": round((my_rays - st.shadow_known) / k_s / 1e6, 3)
+                          if world == 1 else None,
                           "kernel_ms": round(float(np.mean(kernel_ms)), 3),
                           "note": "one frame alone on the GPU (kernel clock); value pipelines "
                                   f"{F} frames in flight"},
-            "work": {"shadow_known_zero": int(st.shadow_known), "bf_queries": int(st.bf_queries),
+            "work": {"shadow_known_zero": int(st.shadow_known), "traced_rays": int(my_rays - st.shadow_known),
+                     "bf_queries": int(st.bf_queries),
                      "stack_spills": int(st.stack_spills), "bvh_build_ms": round(st.bvh_build_ms, 2),
                      "note": "shadow_known_zero: shadow rays counted in value whose cumulative mask was "
-                             "already 0 (result known, not searched); bvh_build_ms: host build before "
-                             "the timed region, not in value"},
+                             "already 0 (result known, not searched; value_traced leaves them out); "
+                             "bvh_build_ms: host build before the timed region, not in value"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "basis": "FLOPs of the ray-box/face/sphere tests the launch executed (kernel "
                                   "counters x flop_per_test) / kernel_ms; replaces SURVEY 8(d)'s brute-force "

@@ -169,8 +169,13 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 //             rounding only (<= 1 ulp per factor); an opaque
 //             hit zeroes the mask whatever the order (early exit when no
 //             factor is NaN).
-// Queries the BVH cannot reproduce (SKIP_TRANS checks, directional shadow
-// rays against spheres) set q.bf and are re-run by the brute-force scan.
+// The reference's two order-dependent cases are answered on the BVH too
+// (DESIGN.md §3.3): a SKIP_TRANS check is the stack top's own nearest root
+// (own_nearest) plus an any-hit search (q.skipchk); a directional shadow ray
+// tests the faces here and the spheres by a cone query in the light's
+// shadow-region tree (bvh_trace<true>).  Only when such a tree could not be
+// built (Params::dir_bf == 1) do directional shadow rays set q.bf and go to
+// the brute-force scan.
 // ---------------------------------------------------------------------------
 // Per-lane counters kept small (VGPR pressure): ray kinds are counted per
 // wave with ballots in the main loop (scalar registers); only the rare events
@@ -1231,7 +1236,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;
     int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
-    if (MODE == MODE_BVH) stk[0] = rtbvh::kEmpty;           // bvh_trace's stack bottom (never overwritten)
+    // bvh_trace's stack bottom: kEmpty, or a refill tag (kRefill + blocks) while
+    // spilled entries wait in device memory (spill / pop); every traversal
+    // leaves it kEmpty
+    if (MODE == MODE_BVH) stk[0] = rtbvh::kEmpty;
     Query q;
     bool busy = false;         // lane owns a pixel
     bool pending = false;      // q holds a finished scan to consume
