@@ -108,8 +108,6 @@ struct Params {
     int W, y0, rows;                     // render `rows` rows of a W-wide image: local row r is
     int rblock, rstep;                   // image row y0 + (r / rblock) * rstep + r % rblock
     unsigned int total;                  // W * rows, or the pixel list's length
-    const int *__restrict__ pix;         // pixel list (x, y pairs; rt_render_pixels) or null: work item k
-                                         // is pixel (pix[2k], pix[2k+1]), its colour goes to out[3k..3k+2]
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
@@ -119,13 +117,15 @@ struct Params {
     int shadow_early_out;                // no NaN shadow factor: an opaque hit ends a shadow ray
     int ovf_stride;                      // BVH: stack spill entries per lane (deepest tree, kSpill multiple)
     int lights_lds;                      // the lights' copy in LDS: float4 offset in rt_lds
-    int nl_lds;                          // lights [0, nl_lds) are in LDS, the rest read from `lights`
     int stack_cap;                       // BVH: stack entries kept in LDS (<= kLdsStack)
     unsigned chunk;                      // work items a wave takes from the counter at a time (0: its idle lanes' count)
     unsigned refill_min;                 // refill only when at least this many lanes are idle (or all are)
     unsigned gate_x;                     // hold reflection/refraction searches until this many lanes have one
     void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
     int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
+    const int *__restrict__ pix;         // pixel list (x, y pairs; rt_render_pixels) or null: work item k
+                                         // is pixel (pix[2k], pix[2k+1]), its colour goes to out[3k..3k+2]
+    int lights_in_lds;                   // 1: the lights are staged in LDS; 0: read from `lights` (too many)
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };

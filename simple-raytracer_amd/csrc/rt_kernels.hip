@@ -624,16 +624,18 @@ extern __shared__ float4 rt_lds[];   // dynamic LDS of render_kernel: state, the
 // then LDS latency, not a dependent trip to L2 (one dependent load per
 // shading step costs ~1 % of C3, profiles/r02/ab_shading_probe.txt)
 //
-// Light i's words (LightK: xyz w | col | L | sdir): from the LDS copy, or from
-// device memory for the lights that did not fit under the workgroup's LDS
-// limit (i >= Params::nl_lds: scenes with thousands of lights).
+// Light i's words (LightK: xyz w | col | L | sdir): from the LDS copy, or --
+// when the scene's lights do not all fit under the workgroup's LDS limit
+// (thousands of lights) -- from device memory.  The condition is a kernel
+// argument, so the branch is a scalar one (a per-lane test cost C3 1 %,
+// profiles/r03/ab_light_fallback.txt).
 struct LightW {
     f4v w0, w1, w2, w3;
 };
 __device__ __forceinline__ LightW light_words(const Params &p, int i) {
     static_assert(sizeof(LightK) == 4 * sizeof(f4v), "LightK = 4 float4");
     LightW r;
-    if (i < p.nl_lds) {
+    if (p.lights_in_lds) {
         const f4v *l = reinterpret_cast<const f4v *>(rt_lds + p.lights_lds) + 4 * i;
         r.w0 = l[0], r.w1 = l[1], r.w2 = l[2], r.w3 = l[3];
     } else {
@@ -1188,7 +1190,11 @@ __device__ __forceinline__ int image_row(const Params &p, int r) {
 // bijection, so the image does not change.
 constexpr int kStrip = 8;   // 4 / 16-row strips: C3 -1.6 / -4 %, C5 -3.7 / -3.9 %
 __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, int &y) {
-    if (p.pix) {                 // a pixel list (rt_render_pixels): image coordinates
+#ifdef RT_AB_NOPIX
+    if (false) {
+#else
+    if (p.pix) {
+#endif                 // a pixel list (rt_render_pixels): image coordinates
         x = p.pix[2 * idx];
         y = p.pix[2 * idx + 1];
         return;
@@ -1223,7 +1229,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         for (int i = threadIdx.x; i < ns4; i += blockDim.x) lds[nf4 + i] = p.sscan[i];
     }
     {
-        const int nl4 = p.nl_lds * (int)(sizeof(LightK) / sizeof(float4));
+        const int nl4 = p.lights_in_lds ? p.nl * (int)(sizeof(LightK) / sizeof(float4)) : 0;
         const float4 *src = reinterpret_cast<const float4 *>(p.lights);
         for (int i = threadIdx.x; i < nl4; i += blockDim.x) rt_lds[p.lights_lds + i] = src[i];
     }
@@ -1322,7 +1328,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
                         q.d = primary_dir(p, px, py);
+#ifdef RT_AB_NOPIX
+                        if (false) {
+#else
                         if (p.pix) {             // the list's k-th colour goes to out[3k..]
+#endif
                             px = (int)idx;
                             py = 0;
                         }

@@ -117,10 +117,10 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
 V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
 // Dynamic LDS of render_kernel: the per-lane shading state, the mode's region
-// (BVH stacks or the staged primitives), then the lights -- as many of them as
-// fit under the device's per-workgroup LDS limit (the rest are read from
-// device memory, Params::nl_lds), so a scene with thousands of lights still
-// renders.
+// (BVH stacks or the staged primitives), then the lights when they all fit
+// under the device's per-workgroup LDS limit (else the kernel reads them from
+// device memory, Params::lights_in_lds: a scene with thousands of lights
+// still renders).
 size_t mode_region_end(const rt_scene *s, int mode) {
     size_t shade = (size_t)kLdsHotWords * kBlock * sizeof(float);    // per-lane shading state
     if (mode == MODE_SCAN_LDS) return shade + s->lds_bytes;
@@ -129,10 +129,10 @@ size_t mode_region_end(const rt_scene *s, int mode) {
 }
 size_t mode_lds_bytes(const rt_scene *s, int mode, Params &p) {
     const size_t end = mode_region_end(s, mode);
-    size_t room = s->max_lds > end ? (s->max_lds - end) / sizeof(LightK) : 0;
-    p.nl_lds = (int)std::min<size_t>((size_t)p.nl, room);
+    const size_t room = s->max_lds > end ? (s->max_lds - end) / sizeof(LightK) : 0;
+    p.lights_in_lds = (size_t)p.nl <= room ? 1 : 0;
     p.lights_lds = (int)(end / sizeof(float4));
-    return end + (size_t)p.nl_lds * sizeof(LightK);
+    return end + (p.lights_in_lds ? (size_t)p.nl * sizeof(LightK) : 0);
 }
 
 // Work items a wave takes from the pixel counter at a time: by default

@@ -570,7 +570,7 @@ def _many_lights_text(n: int) -> str:
 @pytest.mark.parametrize("accel", [0, 1])
 def test_many_lights(accel, tmp_path):
     """3000 lights (192 KB of light records): the lights that do not fit in
-    the workgroup's LDS are read from device memory (Params::nl_lds), so the
+    the workgroup's LDS are read from device memory (Params::lights_in_lds), so the
     scene renders -- the reference has no light limit.  Against the oracle,
     identical ray counts, on both search strategies."""
     (tmp_path / "many.txt").write_text(_many_lights_text(3000))
