@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Multi-GPU balance of the current kernel, measured on ONE GPU: every rank's
+row set of an N-GPU run (interleaved 8-row blocks, rtamd/dist.py) rendered
+alone, both as one frame (kernel clock) and pipelined the way bench.py runs
+N > 1 (frames in flight on the scene's render slots, block slots reserved for
+the gather).  The slowest rank bounds an N-GPU step; the projection assumes
+the ranks do not slow each other down (each has its own GPU) and adds the
+RCCL gather's xGMI time estimate (strip bytes / 153 GB/s per link, SURVEY.md
+§8e).  PROJECTED, not measured on N GPUs.
+
+  python tools/rank_balance.py C3 [--frames 8] [--inflight 4] [--reserve 8]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "simple-raytracer_amd"))
+
+XGMI_GBPS = 153.0          # one xGMI link, per direction
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", nargs="?", default="C3")
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=4)
+    ap.add_argument("--reserve", type=int, default=8)
+    ap.add_argument("--ns", default="1,2,4,8")
+    a = ap.parse_args()
+
+    import torch
+    import rtamd
+    from rtamd import scenes as gen
+    from rtamd.dist import row_set
+
+    d = tempfile.mkdtemp(prefix="rtbal_")
+    path = gen.write_scene(d, a.config)
+    hs = rtamd.HostScene(path, cwd=d)
+    hs.set_depth(gen.CONFIGS[a.config]["depth"])
+    W, H = hs.width, hs.height
+    cam = hs.camera()
+    alone = rtamd.GpuScene(hs)                 # one frame at a time (kernel clock)
+    pipe = rtamd.GpuScene(hs)                  # bench.py's N > 1 setting
+    pipe.set_option("inflight", a.inflight)
+    pipe.set_option("reserve", a.reserve)
+    alone.prepare(cam, W, H)
+    pipe.prepare(cam, W, H)
+    per_max = row_set(H, 1, 0)[4]
+    bufs = [torch.empty((per_max, W, 3), dtype=torch.float32, device="cuda") for _ in range(a.inflight)]
+    streams = [torch.cuda.Stream() for _ in range(a.inflight)]
+    for s in streams:
+        with torch.cuda.stream(s):
+            bufs[0][:1].zero_()
+    torch.cuda.synchronize()
+
+    def pipelined(y0, b, step, nr, frames):
+        def run():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(frames):
+                s = streams[k % a.inflight]
+                pipe.render_row_blocks_async(cam, W, H, y0, b, step, nr, bufs[k % a.inflight].data_ptr(),
+                                             s.cuda_stream)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e3 / frames
+        run()                                  # warm
+        return run()
+
+    out = {"config": a.config, "imsize": [W, H], "frames": a.frames, "inflight": a.inflight,
+           "reserve": a.reserve, "note": "PROJECTED from one GPU: each rank's row set rendered alone; "
+                                          "not measured on N GPUs", "n": {}}
+    base = None
+    for n in (int(v) for v in a.ns.split(",")):
+        ranks = []
+        for r in range(n):
+            y0, b, step, nr, per = row_set(H, n, r)
+            for _ in range(2):
+                alone.render_row_blocks_async(cam, W, H, y0, b, step, nr, bufs[0].data_ptr())
+                st = alone.last_stats()
+            ms_pipe = pipelined(y0, b, step, nr, a.frames)
+            ranks.append(dict(rank=r, rows=nr, rays=st.rays(), kernel_ms=round(st.kernel_ms, 3),
+                              pipelined_ms=round(ms_pipe, 3)))
+            print(n, ranks[-1], flush=True)
+        rays = sum(x["rays"] for x in ranks)
+        k = [x["kernel_ms"] for x in ranks]
+        p = [x["pipelined_ms"] for x in ranks]
+        strip_bytes = row_set(H, n, 0)[4] * W * 3 * 4
+        gather_ms = strip_bytes / (XGMI_GBPS * 1e9) * 1e3 if n > 1 else 0.0
+        step_ms = max(p) + gather_ms           # the gather of frame k overlaps frame k+1 only partly: counted whole
+        ent = dict(ranks=ranks, kernel_ms_max=max(k), kernel_ms_mean=round(sum(k) / n, 3),
+                   balance=round(sum(k) / n / max(k), 3), pipelined_ms_max=max(p),
+                   gather_ms_est=round(gather_ms, 3), projected_step_ms=round(step_ms, 3),
+                   projected_Mrays_per_s=round(rays / step_ms / 1e3, 1))
+        if base is None:
+            base = ent["projected_Mrays_per_s"]
+        ent["projected_speedup"] = round(ent["projected_Mrays_per_s"] / base, 2)
+        out["n"][n] = ent
+        print(n, {kk: v for kk, v in ent.items() if kk != "ranks"}, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
