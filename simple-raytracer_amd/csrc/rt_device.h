@@ -138,15 +138,30 @@ enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 // Largest worst-case BVH stack a tree may need (entries per lane; the spill
 // area is sized per tree, Params::ovf_stride).  Refill tags kRefill + b stay
 // far below the leaf links (> INT_MIN + 256) for b <= kStackMax / kSpill.
-constexpr int kStackMax = 1024;
+constexpr int kStackMax = 512;
 // BVH traversal stack entries per lane in LDS (entry 0: the sentinel); a
 // deeper stack spills its oldest kSpill entries to device memory (rare)
 constexpr int kLdsStack = 16;            // most entries the LDS share may hold (option lds_stack)
-constexpr int kLdsStackDefault = 14;     // 16 (32 KB per block with the shading state): 5 blocks per CU
+#ifndef RT_LDS_STACK
+#define RT_LDS_STACK 14                  // 16 (32 KB per block with the shading state): 5 blocks per CU
                                          // on paper, -8.6 % measured; 14: 270 spills per C3 frame
-constexpr int kSpill = 8;
+#endif
+constexpr int kLdsStackDefault = RT_LDS_STACK;
+#ifndef RT_LDS_STACK_DEEP
+#define RT_LDS_STACK_DEEP 14             // depth > 4 (render_kernel<9 / 17, *>): 16 entries with the
+                                         // lights in device memory (32 KB per block) cost C5 8.5 %
+                                         // (profiles/r03/ab_deep_stack.txt)
+#endif
+constexpr int kLdsStackDeep = RT_LDS_STACK_DEEP;
+#ifndef RT_SPILL
+#define RT_SPILL 8
+#endif
+constexpr int kSpill = RT_SPILL;
 static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack - 3 > kSpill, "stack spill blocks");
-constexpr int kBlock = 256;
+#ifndef RT_BLOCK
+#define RT_BLOCK 256                     // lanes per workgroup of render_kernel
+#endif
+constexpr int kBlock = RT_BLOCK;
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 constexpr int kNStats = 40;              // device counter slots (rt_scene_debug_counters)
 constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS (rt_kernels.hip LW_*)

@@ -57,6 +57,7 @@ struct rt_scene {
     size_t max_lds = 64 * 1024;        // the device's LDS limit per workgroup
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
+    long long opt_lds_stack = -1;      // BVH stack entries in LDS (-1: by depth, launch)
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_chunk = -1;          // refill chunk (-1: default, chunk_for)
     long long opt_refill_min = -1;     // idle lanes before a refill (-1: by the scene, refill_for)
@@ -121,18 +122,21 @@ V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 // under the device's per-workgroup LDS limit (else the kernel reads them from
 // device memory, Params::lights_in_lds: a scene with thousands of lights
 // still renders).
-size_t mode_region_end(const rt_scene *s, int mode) {
+size_t mode_region_end(const rt_scene *s, int mode, const Params &p) {
     size_t shade = (size_t)kLdsHotWords * kBlock * sizeof(float);    // per-lane shading state
     if (mode == MODE_SCAN_LDS) return shade + s->lds_bytes;
-    if (mode == MODE_BVH) return shade + (size_t)s->base.stack_cap * kBlock * sizeof(int);
+    if (mode == MODE_BVH) return shade + (size_t)p.stack_cap * kBlock * sizeof(int);
     return shade;
 }
-size_t mode_lds_bytes(const rt_scene *s, int mode, Params &p) {
-    const size_t end = mode_region_end(s, mode);
-    const size_t room = s->max_lds > end ? (s->max_lds - end) / sizeof(LightK) : 0;
-    p.lights_in_lds = (size_t)p.nl <= room ? 1 : 0;
+// The launch's dynamic LDS; decides Params::lights_in_lds: the lights are
+// staged when they fit under the limit and do not cost a resident workgroup
+// per CU (by the occupancy calculator), else they come from device memory.
+size_t mode_lds_bytes(const rt_scene *s, int maxf, int mode, Params &p) {
+    const size_t end = mode_region_end(s, mode, p);
+    const size_t with = end + (size_t)p.nl * sizeof(LightK);
     p.lights_lds = (int)(end / sizeof(float4));
-    return end + (p.lights_in_lds ? (size_t)p.nl * sizeof(LightK) : 0);
+    p.lights_in_lds = with <= s->max_lds && render_blocks_per_cu(maxf, mode, with) >= render_blocks_per_cu(maxf, mode, end);
+    return p.lights_in_lds ? with : end;
 }
 
 // Work items a wave takes from the pixel counter at a time: by default
@@ -159,7 +163,7 @@ static unsigned refill_for(const rt_scene *s, const Params &p) {
 
 hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, int mode, hipStream_t st, bool dry) {
     Params pl = p;
-    size_t shm = mode_lds_bytes(s, mode, pl);
+    size_t shm = mode_lds_bytes(s, maxf, mode, pl);
     int nb = render_blocks_per_cu(maxf, mode, shm);
     if (nb < 1) nb = 1;
     long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu - s->opt_reserve;
@@ -498,7 +502,12 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
         if (s->lds_bytes > 64 * 1024) lds = false;
         if (lds) mode = MODE_SCAN_LDS;
     }
-    if (mode == MODE_SCAN_LDS && mode_region_end(s, MODE_SCAN_LDS) > s->max_lds) mode = MODE_SCAN;
+    if (mode == MODE_SCAN_LDS && mode_region_end(s, MODE_SCAN_LDS, p) > s->max_lds) mode = MODE_SCAN;
+    // BVH stack entries in LDS (option lds_stack, else per instantiation): 16
+    // cost C3 8.6 % with the lights staged and 10 % without, C5 8.5 %: a
+    // workgroup above ~31 KB of LDS loses a resident workgroup per CU in
+    // practice (profiles/r02/ab_lds_stack.txt, profiles/r03/ab_deep_stack.txt)
+    p.stack_cap = s->opt_lds_stack > 0 ? (int)s->opt_lds_stack : depth > 4 ? kLdsStackDeep : kLdsStackDefault;
     hipError_t e = launch_one(s, slot, p, maxf_for_depth(depth), mode, st, dry);
     return e == hipSuccess ? RT_OK : RT_E_HIP;
 }
@@ -780,7 +789,6 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.depth = desc->depth;
     p.dir_bf = 0;                      // set with the BVH (build_bvh); the scan needs none
     p.shadow_early_out = nan_fac ? 0 : 1;
-    p.stack_cap = kLdsStackDefault;
     p.chunk = 0;                       // launch_one: chunk_for, refill_for
     p.refill_min = 1;
     p.gate_x = kGateX;
@@ -831,8 +839,8 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         s->opt_chunk = value;
     }
     else if (k == "lds_stack") {
-        if (value < 12 || value > kLdsStack) return RT_E_INVALID;
-        s->base.stack_cap = (int)value;
+        if (value < kSpill + 4 || value > kLdsStack) return RT_E_INVALID;
+        s->opt_lds_stack = value;
     }
     else if (k == "bvh_leaf" || k == "bvh_trav" || k == "bvh_collapse" || k == "bvh_node") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
