@@ -334,7 +334,9 @@ def main() -> None:
                           if world > 1 else ""), "frames_in_flight": F,
                        "reserved_block_slots": reserve,
                        "launch": {"blocks_per_cu": int(dbg[17]), "grid": int(dbg[18]),
-                                  "lds_bytes_per_block": int(dbg[19]), "bvh_nodes": int(dbg[20])}},
+                                  "lds_bytes_per_block": int(dbg[19]), "bvh_nodes": int(dbg[20]),
+                                  "lds_stack": int(dbg[42]), "lights_in_lds": int(dbg[43]),
+                                  "org_first": int(dbg[40]), "scene_density": round(dbg[41] / 1000, 2)}},
             "one_frame": {"Mrays_per_s": round(my_rays / k_s / 1e6, 3) if world == 1 else None,
                           "Mrays_per_s_traced": round((my_rays - st.shadow_known) / k_s / 1e6, 3)
                           if world == 1 else None,

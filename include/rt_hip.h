@@ -215,6 +215,9 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * (0..64, default 32: reflection / refraction searches wait until that many
  * lanes of the wave have one, unless nothing else would search) -- neither
  * changes the image,
+ * "org_first" (-1 auto, or bits 1 shadow / 2 refraction / 4 reflection rays:
+ * test the ray's origin object's BVH leaf before the search from the root;
+ * auto = 6 in dense scenes, else 0 -- never changes the image),
  * "fail_bvh_upload" (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
@@ -229,7 +232,10 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * spills (as in rt_stats), [35] BVH queries with a NaN origin or direction
  * (no hit; not searched); RT_PROF builds: [36..38] traversal trips of primary /
  * shadow / refraction + reflection queries, [39] trace steps whose wave searched
- * primary and other rays together.  n <= 40. */
+ * primary and other rays together; more launch facts: [40] origin-leaf pass
+ * bits in effect (option org_first), [41] the scene's density (objects a line
+ * across it meets, x1000), [42] BVH stack entries in LDS, [43] lights staged
+ * in LDS (1) or read from device memory (0).  n <= 48. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);

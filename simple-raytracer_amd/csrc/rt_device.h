@@ -126,6 +126,8 @@ struct Params {
     const int *__restrict__ pix;         // pixel list (x, y pairs; rt_render_pixels) or null: work item k
                                          // is pixel (pix[2k], pix[2k+1]), its colour goes to out[3k..3k+2]
     int lights_in_lds;                   // 1: the lights are staged in LDS; 0: read from `lights` (too many)
+    const int *__restrict__ objleaf;     // BVH: per object, the link of its leaf in the main tree
+    int org_first;                       // origin-leaf pass: bit 0 shadow, 1 refraction, 2 reflection rays
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -163,7 +165,13 @@ static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack -
 #endif
 constexpr int kBlock = RT_BLOCK;
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
-constexpr int kNStats = 40;              // device counter slots (rt_scene_debug_counters)
+#ifndef RT_ORG_FIRST
+#define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /
+                                         // reflection (4) rays -- in scenes denser than kOrgDensity
+#endif
+constexpr int kOrgFirst = RT_ORG_FIRST;
+constexpr double kOrgDensity = 32.0;     // objects met by a line across the scene (C3 ~3, C5 ~200)
+constexpr int kNStats = 48;              // counter slots (rt_scene_debug_counters; the device writes 0..39)
 constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS (rt_kernels.hip LW_*)
 
 // ---------------------------------------------------------------------------

@@ -70,7 +70,9 @@ struct Query {
 constexpr float kInf = __builtin_huge_valf();
 
 __device__ __forceinline__ void offer(Query &q, float t, int obj, const float *__restrict__ ofac) {
-    bool in = (t > q.tmin) & ((t < q.tmax) | q.unb) & (obj != q.self);
+    // (closest queries carry their origin object in q.self for the BVH's
+    // origin-leaf pass, bvh_trace; they never exclude it)
+    bool in = (t > q.tmin) & ((t < q.tmax) | q.unb) & (q.closest | (obj != q.self));
     if (in) {
         if (q.closest) {
             if (q.skipchk & (obj != q.back)) {
@@ -239,6 +241,12 @@ __device__ __forceinline__ float safe_rcp(float x) {
 // One leaf's primitives against q: faces (5 words each) then spheres (2 words),
 // rt_bvh.h leaf_records.  Closest: running (best, win); shadow: every valid
 // hit multiplies the mask (an opaque one ends the ray).
+//
+// PRE: the origin-leaf pass (bvh_trace): a shadow query only looks for an
+// opaque occluder there (its other factors are multiplied by the full search
+// that follows, which visits this leaf again); closest and SKIP queries are
+// idempotent under a repeated candidate and run as usual.
+template <bool PRE = false>
 __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, Counters &cnt, float &best, int &win,
                                            bool &opaque, bool faces_only) {
     int v = -link - 1;
@@ -294,7 +302,7 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
             } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
                 if (fac == 0.0f && p.shadow_early_out) {
                     opaque = true;
-                } else {
+                } else if (!PRE) {
                     q.mask = cmulf(q.mask, fac);
                 }
             }
@@ -374,8 +382,10 @@ __device__ __forceinline__ float child_entry(const ChildPlanes &cp, int i, float
 // the plane distances are the child boxes' offsets from po, and a cone test
 // per child instead of the slab test; its leaves are still tested with the
 // query's own ray (q.o, q.d).
+//
+// org_pass: run the origin-leaf pass first (option org_first, by ray kind).
 template <bool point, unsigned LEAF_WAIT = kLeafWait>
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, int root = 0,
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bool org_pass = false, int root = 0,
                           V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
     // |1/d| capped at 2^100 (1/0 -> 1e30 as before): the quantised planes'
     // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
@@ -511,9 +521,21 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, in
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
     // (loads and stores share vmcnt, in order).
+    // Origin-leaf pass (org_pass; option org_first): a secondary ray starts on an
+    // object, and in a dense scene what it meets first is often in that
+    // object's own leaf -- a refraction ray entering a sphere meets the
+    // sphere's far side, a reflection or shadow ray a neighbour.  The leaf is
+    // tested before the search from the root: a closest hit found there bounds
+    // the search (thi), an opaque occluder ends a shadow ray.  The search
+    // visits the leaf again; that changes no result (PRE, leaf_visit).
+    bool ended = false;
+    if (!point && org_pass && !faces_only && !q.skipchk && q.self >= 0 && (q.closest || p.shadow_early_out)) {
+        leaf_visit<true>(q, p, p.objleaf[q.self], cnt, best, win, opaque, false);
+        ended = opaque;
+    }
     if (point)
         node = root;
-    else
+    else if (!ended)
         visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4));
     for (;;) {
         while (node >= 0) {
@@ -1006,12 +1028,12 @@ __device__ __forceinline__ void shadow_query(Query &q, const Params &p, int ligh
     q.win = -1;
 }
 
-__device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d) {
+__device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d, int org) {
     q.d = d;
     q.tmin = p.eps;
     q.tmax = kFltMax;
     q.unb = false;
-    q.self = -1;
+    q.self = org;                    // origin object (not excluded: offer)
     q.closest = true;
     q.skipchk = false;
     q.skipped = false;
@@ -1132,7 +1154,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             if (p.depth - top > 0 && !tir && (double)ob.opacity < 1.0 && ob.eta > 0) {
                 float k = sqrtf((float)(1.0 - (double)(snell * snell) * (1.0 - (double)(cosI * cosI))));
                 V3 T = vadd(vmul(vmul(h.N, -1.0f), k), vmul(vsub(vmul(h.N, cosI), h.I), snell));
-                closest_query(q, p, T);
+                closest_query(q, p, T, h.obj);
                 const int sn = h_sn(h);
                 q.skipchk = (sn > 0) && !ob.is_sphere;
                 q.back = sn > 0 ? (top == 0 ? h.obj : ls.cold()[top - 1].stack[sn - 1]) : -1;
@@ -1148,7 +1170,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             float Fr = refl_fresnel(ob, cosI);
             if (p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
                 V3 R = vsub(vmul(h.N, (float)(2.0 * (double)cosI)), h.I);
-                closest_query(q, p, R);
+                closest_query(q, p, R, h.obj);
                 lds_store_phase(h);
                 ls.top = top;
                 return RK_REFL;
@@ -1404,7 +1426,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_lanes += (unsigned long long)__popcll(__ballot(search && !q.bf));
             unsigned tr0 = cnt.trips;
 #endif
-            if (search && !q.bf) bvh_trace<false, leaf_wait_for(MAXF)>(q, p, stk, cnt);
+            // origin-leaf pass by the query's kind (held_kind: this step's):
+            // bit 0 shadow, 1 refraction, 2 reflection rays
+            const bool org_pass = held_kind >= RK_SHADOW && held_kind <= RK_REFL &&
+                                  ((p.org_first >> (held_kind - RK_SHADOW)) & 1);
+            if (search && !q.bf) bvh_trace<false, leaf_wait_for(MAXF)>(q, p, stk, cnt, org_pass);
             if (skip) {
                 q.closest = true;
                 q.unb = false;
@@ -1423,7 +1449,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                         V3 po = {fmaf(dk.R[0], q.o.x, fmaf(dk.R[1], q.o.y, dk.R[2] * q.o.z)),
                                  fmaf(dk.R[3], q.o.x, fmaf(dk.R[4], q.o.y, dk.R[5] * q.o.z)),
                                  fmaf(dk.R[6], q.o.x, fmaf(dk.R[7], q.o.y, dk.R[8] * q.o.z))};
-                        bvh_trace<true>(q, p, stk, cnt, root, po, dk.cone_k, dk.cone_h);
+                        bvh_trace<true>(q, p, stk, cnt, false, root, po, dk.cone_k, dk.cone_h);
                     }
                 }
             }

@@ -58,6 +58,8 @@ struct rt_scene {
     size_t lds_bytes = 0;
     long long opt_lds = -1;            // -1 auto, 0 off, 1 on
     long long opt_lds_stack = -1;      // BVH stack entries in LDS (-1: by depth, launch)
+    double crossings = 0.0;            // objects a line across the scene meets on average (org_first)
+    int org_first_auto = 0;            // org_first by that density
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_chunk = -1;          // refill chunk (-1: default, chunk_for)
     long long opt_refill_min = -1;     // idle lanes before a refill (-1: by the scene, refill_for)
@@ -84,6 +86,7 @@ struct rt_scene {
     float4 *d_bvh = nullptr;
     float4 *d_leafrec = nullptr;
     DirK *d_dirk = nullptr;            // per light: shadow-region tree (directional lights)
+    int *d_objleaf = nullptr;          // per object: its leaf's link in the main tree
     std::vector<float4> h_fscan, h_sscan;   // host copies for the leaf records
     std::vector<float> h_ofac;
     std::vector<LightK> h_lights;
@@ -94,6 +97,7 @@ struct rt_scene {
     bool bvh_ok = false;
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
+    long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0;
     long long bvh_nodes = 0;
     bool last_valid = false;
 };
@@ -192,6 +196,9 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     s->last_grid = grid;
     s->last_lds = (long long)shm;
     s->last_mode = mode;
+    s->last_org_first = pl.org_first;
+    s->last_stack_cap = pl.stack_cap;
+    s->last_lights_in_lds = pl.lights_in_lds;
     if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
     return render_launch(maxf, mode, pl, (unsigned)grid, shm, st);
 }
@@ -397,6 +404,26 @@ int build_bvh(rt_scene *s, double D) {
             return 2;
         });
     rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
+    // every object's leaf in the main tree (the origin-leaf pass, bvh_trace)
+    std::vector<int32_t> objleaf((size_t)std::max(1, nf + s->base.ns), rtbvh::kEmptyLeaf);
+    if (ok)
+        for (const auto &n : Q.nodes)
+            for (int32_t l : n.link) {
+                if (l >= 0 || l == rtbvh::kEmpty) continue;
+                const int v = -l - 1, nfc = (v >> 4) & 15, count = v & 15;
+                size_t off = (size_t)(v >> 8);
+                for (int k = 0; k < count; k++) {
+                    int32_t key;
+                    if (k < nfc) {
+                        memcpy(&key, &rec[off + 4].y, sizeof key);
+                        off += 5;
+                    } else {
+                        memcpy(&key, &rec[off + 1].x, sizeof key);
+                        off += 2;
+                    }
+                    objleaf[(size_t)key] = l;
+                }
+            }
     std::vector<rtbvh::Node4H> QQ;
     if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ)) ok = false;     // non-finite geometry: scan
     for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
@@ -426,6 +453,7 @@ int build_bvh(rt_scene *s, double D) {
     // pointers and no tree marked valid that is not there).
     float4 *nb = nullptr, *nr = nullptr;
     DirK *nd = nullptr;
+    int *nl = nullptr;
     int rc = RT_OK;
     if (ok && s->opt_fail_bvh_upload) {        // test hook: as if the device allocation failed
         rc = RT_E_NOMEM;
@@ -436,31 +464,37 @@ int build_bvh(rt_scene *s, double D) {
         const size_t dir_bytes = std::max<size_t>(1, dirk.size()) * sizeof(DirK);
         if (hipMalloc(&nb, node_bytes) != hipSuccess ||
             hipMalloc(&nr, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess ||
-            hipMalloc(&nd, dir_bytes) != hipSuccess)
+            hipMalloc(&nd, dir_bytes) != hipSuccess || hipMalloc(&nl, objleaf.size() * sizeof(int32_t)) != hipSuccess)
             rc = RT_E_NOMEM;
         else if (hipMemcpy(nb, QQ.data(), node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
                  hipMemcpy(nr, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess ||
                  (!dirk.empty() && hipMemcpy(nd, dirk.data(), dirk.size() * sizeof(DirK), hipMemcpyHostToDevice) !=
-                                       hipSuccess))
+                                       hipSuccess) ||
+                 hipMemcpy(nl, objleaf.data(), objleaf.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
             rc = RT_E_HIP;
         if (rc) {
             if (nb) (void)hipFree(nb);
             if (nr) (void)hipFree(nr);
             if (nd) (void)hipFree(nd);
+            if (nl) (void)hipFree(nl);
             nb = nr = nullptr;
             nd = nullptr;
+            nl = nullptr;
         }
     }
     // renders still queued may read the old tree: free it after they finish
-    if (s->d_bvh || s->d_leafrec || s->d_dirk) {
+    if (s->d_bvh || s->d_leafrec || s->d_dirk || s->d_objleaf) {
         (void)hipDeviceSynchronize();
         if (s->d_bvh) (void)hipFree(s->d_bvh);
         if (s->d_leafrec) (void)hipFree(s->d_leafrec);
         if (s->d_dirk) (void)hipFree(s->d_dirk);
+        if (s->d_objleaf) (void)hipFree(s->d_objleaf);
     }
     s->d_bvh = nb;
     s->d_leafrec = nr;
     s->d_dirk = nd;
+    s->d_objleaf = nl;
+    s->base.objleaf = nl;
     s->base.bvh = nb;
     s->base.leafrec = nr;
     s->base.dirk = nd;
@@ -493,6 +527,7 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
             p.bvh = s->base.bvh;
             p.leafrec = s->base.leafrec;
             p.dirk = s->base.dirk;
+            p.objleaf = s->base.objleaf;
             p.dir_bf = s->base.dir_bf;
             p.ovf_stride = s->ovf_stride;
         }
@@ -792,6 +827,28 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.chunk = 0;                       // launch_one: chunk_for, refill_for
     p.refill_min = 1;
     p.gate_x = kGateX;
+    // The origin-leaf pass for reflection and refraction rays pays in dense
+    // scenes (C5: +2.3 %) and costs sparse ones (C3: -1.1 %;
+    // profiles/r03/ab_origin_leaf.txt).  Density here: the objects a straight
+    // line across the scene's box meets on average -- total cross-section
+    // (spheres pi r^2, triangles area / 2, averaged over directions) per
+    // volume, times the box diagonal (C3: ~3, C5: ~200).
+    {
+        double xs = 0.0, vol = 1.0, diag2 = 0.0;
+        for (int i = 0; i < nf; i++) {
+            V3 c = vcross(f3(&fscan[5 * i + 2].x), f3(&fscan[5 * i + 3].x));
+            xs += 0.25 * std::sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z);
+        }
+        for (int i = 0; i < ns; i++) xs += kPi * (double)sscan[i].w * (double)sscan[i].w;
+        for (int k = 0; k < 3; k++) {
+            const double e = (double)s->scene_hi[k] - (double)s->scene_lo[k];
+            vol *= e;
+            diag2 += e * e;
+        }
+        s->crossings = vol > 0.0 && std::isfinite(xs) ? xs / vol * std::sqrt(diag2) : 0.0;
+        s->org_first_auto = s->crossings > kOrgDensity ? kOrgFirst : 0;
+        p.org_first = s->org_first_auto;
+    }
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
     *out = s;
     return RT_OK;
@@ -808,6 +865,7 @@ int rt_scene_destroy(rt_scene *s) {
     if (s->d_bvh) (void)hipFree(s->d_bvh);
     if (s->d_leafrec) (void)hipFree(s->d_leafrec);
     if (s->d_dirk) (void)hipFree(s->d_dirk);
+    if (s->d_objleaf) (void)hipFree(s->d_objleaf);
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->dev_pix) (void)hipFree(s->dev_pix);
     for (auto &r : s->slots) free_slot(r);
@@ -826,6 +884,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "accel") s->opt_accel = value;
     else if (k == "inflight") return set_inflight(s, value);
     else if (k == "fail_bvh_upload") s->opt_fail_bvh_upload = value;
+    else if (k == "org_first") {
+        if (value < -1 || value > 7) return RT_E_INVALID;
+        s->base.org_first = value < 0 ? s->org_first_auto : (int)value;
+    }
     else if (k == "gate_x") {
         if (value < 0 || value > 64) return RT_E_INVALID;
         s->base.gate_x = (unsigned)value;
@@ -1004,6 +1066,10 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[21] = (unsigned long long)s->bvh_depth;
     h[22] = (unsigned long long)s->bvh_stack;
     h[23] = (unsigned long long)s->num_cu;
+    h[40] = (unsigned long long)s->last_org_first;
+    h[41] = (unsigned long long)(s->crossings * 1000.0);
+    h[42] = (unsigned long long)s->last_stack_cap;
+    h[43] = (unsigned long long)s->last_lights_in_lds;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }

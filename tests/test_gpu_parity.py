@@ -704,6 +704,51 @@ def test_extreme_batching_deep_scene(opts):
     assert _counts(st) == cnt
 
 
+def test_origin_leaf_pass_bit_identical():
+    """Option org_first: a secondary ray first tests the BVH leaf of the object
+    it starts on (a closest hit found there bounds the search, an opaque
+    occluder there ends a shadow ray), then searches from the root.  Images
+    and ray counts are bit for bit those without it, for every combination of
+    ray kinds, on C3 (2000 objects, glass), C3G (glass triangles: SKIP_TRANS),
+    C5 (100 000 spheres, depth 8) and test7 (NaN pixels); the automatic
+    setting turns it on for C5's dense scene and off for C3."""
+    cases = [("C3_64x64.txt", 4, SCENES), ("C5_8x8.txt", 8, SCENES), ("test7_s.txt", 4, SCENES)]
+    for name, depth, cwd in cases:
+        hs = rtamd.HostScene(name, cwd=cwd)
+        hs.set_depth(depth)
+        W, H = hs.width, hs.height
+        cam = hs.camera()
+        ref = None
+        for v in (0, 1, 2, 4, 7, -1):
+            gs = rtamd.GpuScene(hs)
+            gs.set_option("accel", 1)
+            gs.set_option("org_first", v)
+            img, st = gs.render_rows(cam, W, H, 0, H)
+            dbg = gs.debug_counters()
+            if ref is None:
+                ref = (img, _counts(st))
+            assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref[0], nan=-9)), (name, v)
+            assert _counts(st) == ref[1], (name, v)
+            if v == -1:
+                auto = int(dbg[40])
+                assert auto == (6 if name.startswith("C5") else 0), (name, auto, dbg[41] / 1000)
+                _summary[f"org_first_auto_{name}"] = dict(org_first=auto, density=dbg[41] / 1000)
+            gs.close()
+
+
+def test_origin_leaf_pass_special_cases(tmp_path):
+    """The origin-leaf pass on the reference's order-dependent cases: glass
+    triangles (SKIP_TRANS) and a directional light over spheres (cone
+    queries), all ray kinds on, against the oracle with identical counts."""
+    for cfg in ("C3G", "C3D"):
+        name = f"{cfg}_40x32.txt"
+        (tmp_path / name).write_text(gen.scene_text(cfg, w=40, h=32))
+        img, st = rtamd.render_scene(name, cwd=str(tmp_path), options={"org_first": 7})
+        ref, cnt = OracleScene(name, cwd=str(tmp_path)).render()
+        assert_parity(img, ref, f"{cfg} org_first=7")
+        assert _counts(st) == cnt
+
+
 @pytest.mark.parametrize("opts", [{"bvh_collapse": 0}, {"bvh_collapse": 1, "bvh_node": 1000}])
 def test_bvh_collapse_parity(opts):
     """The 4-wide tree comes from the binary SAH tree by an SAH-optimal
