@@ -740,33 +740,42 @@ __device__ __forceinline__ V3 cold_restore(const Cold<MAXF> &c, HotR &h) {
     return V3{c.P[0], c.P[1], c.P[2]};
 }
 
-// Hit record of the winning intersection, recomputed exactly as TraceRay did.
-__device__ void hit_geometry(const Params &p, int obj, V3 o, V3 d, float t, V3 &P, V3 &N, V3 &bary) {
-    P = vadd(o, vmul(d, t));
+// Hit record of the winning intersection, recomputed exactly as TraceRay did:
+// the point, the normal and (faces) the barycentric coordinates.  Plain
+// scalars, not out-parameters: a V3 written in two branches through a
+// reference was kept in scratch (a store and a reload per node open).
+struct HitRec {
+    V3 P, N;
+    float ba, bb, bg;
+};
+__device__ __forceinline__ HitRec hit_geometry(const Params &p, int obj, V3 o, V3 d, float t) {
+    HitRec h;
+    h.P = vadd(o, vmul(d, t));
+    h.ba = h.bb = h.bg = 0.0f;
     if (obj < p.nf) {
         const float4 *F = p.fscan + 5 * obj;
         float4 f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4];
-        V3 ep = vsub(P, V3{f0.x, f0.y, f0.z});
+        V3 ep = vsub(h.P, V3{f0.x, f0.y, f0.z});
         V3 e1 = {f2.x, f2.y, f2.z}, e2 = {f3.x, f3.y, f3.z};
         float d1p = vdot(e1, ep), d2p = vdot(e2, ep);
         float b = (f3.w * d1p - f4.x * d2p) / f1.w;
         float g = (f2.w * d2p - f4.x * d1p) / f1.w;
         float a = 1.0f - (b + g);
-        bary = {a, b, g};
+        h.ba = a, h.bb = b, h.bg = g;
         const FaceShadeK &fs = p.fsh[obj];
         if (fs.smooth) {
             V3 n0 = {fs.vn[0][0], fs.vn[0][1], fs.vn[0][2]};
             V3 n1 = {fs.vn[1][0], fs.vn[1][1], fs.vn[1][2]};
             V3 n2 = {fs.vn[2][0], fs.vn[2][1], fs.vn[2][2]};
-            N = vnorm(vadd(vadd(vmul(n0, a), vmul(n1, b)), vmul(n2, g)));
+            h.N = vnorm(vadd(vadd(vmul(n0, a), vmul(n1, b)), vmul(n2, g)));
         } else {
-            N = {f1.x, f1.y, f1.z};
+            h.N = {f1.x, f1.y, f1.z};
         }
     } else {
         float4 s = p.sscan[obj - p.nf];
-        N = vnorm(vdiv(vsub(P, V3{s.x, s.y, s.z}), s.w));
-        bary = {0, 0, 0};
+        h.N = vnorm(vdiv(vsub(h.P, V3{s.x, s.y, s.z}), s.w));
     }
+    return h;
 }
 
 // Texel (x, y) of a texture, channel c -- the reference's nearest texel
@@ -858,8 +867,9 @@ struct Medium {
 };
 
 __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m) {
-    V3 P, N, bary;
-    hit_geometry(p, obj, o, d, t, P, N, bary);
+    const HitRec hr = hit_geometry(p, obj, o, d, t);
+    const V3 P = hr.P;
+    V3 N = hr.N;
     const ObjK &ob = p.objs[obj];
     V3 I = vmul(d, -1.0f);
     float cosI = vdot(N, I);
@@ -880,8 +890,8 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
             dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
         } else {                                                     // main.cpp:834-861
             const FaceShadeK &fs = p.fsh[obj];
-            float u = (bary.x * fs.vt[0][0]) + (bary.y * fs.vt[1][0]) + (bary.z * fs.vt[2][0]);
-            float v = (bary.x * fs.vt[0][1]) + (bary.y * fs.vt[1][1]) + (bary.z * fs.vt[2][1]);
+            float u = (hr.ba * fs.vt[0][0]) + (hr.bb * fs.vt[1][0]) + (hr.bg * fs.vt[2][0]);
+            float v = (hr.ba * fs.vt[0][1]) + (hr.bb * fs.vt[1][1]) + (hr.bg * fs.vt[2][1]);
             v = clampr(v, 0.0f, 1.0f);
             u = clampr(u, 0.0f, 1.0f);
             int i = (int)clampr(roundf((width - 1.0f) * u), 0.0f, (float)((double)width - 1.0));

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=4)
     ap.add_argument("--reserve", type=int, default=8)
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--option", action="append", default=[], help="kernel option key=value (both scenes)")
     a = ap.parse_args()
 
     import torch
@@ -49,6 +50,10 @@ def main():
     pipe = rtamd.GpuScene(hs)                  # bench.py's N > 1 setting
     pipe.set_option("inflight", a.inflight)
     pipe.set_option("reserve", a.reserve)
+    for kv in a.option:
+        k, v = kv.split("=")
+        alone.set_option(k, int(v))
+        pipe.set_option(k, int(v))
     alone.prepare(cam, W, H)
     pipe.prepare(cam, W, H)
     per_max = row_set(H, 1, 0)[4]
@@ -73,7 +78,7 @@ def main():
         return run()
 
     out = {"config": a.config, "imsize": [W, H], "frames": a.frames, "inflight": a.inflight,
-           "reserve": a.reserve, "note": "PROJECTED from one GPU: each rank's row set rendered alone; "
+           "reserve": a.reserve, "options": a.option, "note": "PROJECTED from one GPU: each rank's row set rendered alone; "
                                           "not measured on N GPUs", "n": {}}
     base = None
     for n in (int(v) for v in a.ns.split(",")):
