@@ -32,6 +32,17 @@
 
 namespace rt {
 
+// RT_COUNT_TESTS 0: the executed-test counters are compiled out (A/B of their
+// register cost; rt_stats' box/face/sphere tests are then 0)
+#ifndef RT_COUNT_TESTS
+#define RT_COUNT_TESTS 1
+#endif
+#if RT_COUNT_TESTS
+#define RT_COUNT(x) (x)
+#else
+#define RT_COUNT(x) ((void)0)
+#endif
+
 // Read-only scene data seen through the constant address space: the loads
 // are wave-uniform and invariant, so they become scalar (s_load) reads into
 // SGPRs through the scalar cache instead of 64 identical per-lane loads.
@@ -48,6 +59,16 @@ __device__ __forceinline__ float4 sld4(const float4 *p, int i) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+
+// Row i of a per-object array, addressed where it is read: the opaque index
+// keeps LLVM from computing the 64-bit address once and holding it in a VGPR
+// pair across the shading code (where it was spilled to scratch and reloaded
+// every step); recomputing it is two VALU instructions.
+template <typename T>
+__device__ __forceinline__ const T &row(const T *base, int i) {
+    asm volatile("" : "+v"(i));
+    return base[i];
+}
 
 // ---------------------------------------------------------------------------
 // One lane's ray query (a TraceRay call + the consumer loop that follows it)
@@ -130,8 +151,8 @@ template <bool SRC_LDS>
 __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s,
                                      bool part, unsigned &ft, unsigned &st) {
     if (!part) return;
-    ft += (unsigned)p.nf;
-    st += (unsigned)p.ns;
+    RT_COUNT(ft += (unsigned)p.nf);
+    RT_COUNT(st += (unsigned)p.ns);
     for (int i = 0; i < p.nf; i++) {
         float4 f0, f1, f2, f3, f4;
         if (SRC_LDS) {
@@ -203,13 +224,13 @@ __device__ __forceinline__ float own_nearest(const Query &q, const Params &p, in
     if (obj < p.nf) {
         const float4 *F = p.fscan + 5 * obj;
         float t, a, b, g;
-        cnt.ftests++;
+        RT_COUNT(cnt.ftests++);
         if (face_test(F[0], F[1], F[2], F[3], F[4], q.o, q.d, t, a, b, g) & (F[1].w != 0.0f) & (t > q.tmin) &
             (t < kFltMax))
             tb = t;
     } else {
         float t1, t2;
-        cnt.stests++;
+        RT_COUNT(cnt.stests++);
         if (sphere_test(p.sscan[obj - p.nf], q.o, q.d, t1, t2)) {
             if ((t1 > q.tmin) & (t1 < tb)) tb = t1;
             if ((t2 > q.tmin) & (t2 < tb)) tb = t2;
@@ -274,13 +295,13 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
             key = __float_as_int(f4.y);
             fac = f4.z;
             float a, bb, g;
-            cnt.ftests++;
+            RT_COUNT(cnt.ftests++);
             if (face_test(f0, f1, f2, f3, f4, q.o, q.d, t[0], a, bb, g) & (f1.w != 0.0f)) nt = 1;
         } else {
             R += 2;
             key = __float_as_int(f1.x);
             fac = f1.y;
-            cnt.stests++;
+            RT_COUNT(cnt.stests++);
             if (sphere_test(f0, q.o, q.d, t[0], t[1])) nt = 2;
         }
         for (int r = 0; r < nt; r++) {
@@ -455,7 +476,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
 #if RT_PROF
         cnt.trips++;
 #endif
-        cnt.boxes += 4;
+        RT_COUNT(cnt.boxes += 4);
         float thi = thi_now();
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
         const ChildPlanes cp = child_planes(w0, w1, w2, w3, ix, iy, iz, ox, oy, oz, neg_x, neg_y, neg_z);
@@ -753,7 +774,7 @@ __device__ __forceinline__ HitRec hit_geometry(const Params &p, int obj, V3 o, V
     h.P = vadd(o, vmul(d, t));
     h.ba = h.bb = h.bg = 0.0f;
     if (obj < p.nf) {
-        const float4 *F = p.fscan + 5 * obj;
+        const float4 *F = &row(p.fscan, 5 * obj);
         float4 f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4];
         V3 ep = vsub(h.P, V3{f0.x, f0.y, f0.z});
         V3 e1 = {f2.x, f2.y, f2.z}, e2 = {f3.x, f3.y, f3.z};
@@ -762,7 +783,7 @@ __device__ __forceinline__ HitRec hit_geometry(const Params &p, int obj, V3 o, V
         float g = (f2.w * d2p - f4.x * d1p) / f1.w;
         float a = 1.0f - (b + g);
         h.ba = a, h.bb = b, h.bg = g;
-        const FaceShadeK &fs = p.fsh[obj];
+        const FaceShadeK &fs = row(p.fsh, obj);
         if (fs.smooth) {
             V3 n0 = {fs.vn[0][0], fs.vn[0][1], fs.vn[0][2]};
             V3 n1 = {fs.vn[1][0], fs.vn[1][1], fs.vn[1][2]};
@@ -772,7 +793,7 @@ __device__ __forceinline__ HitRec hit_geometry(const Params &p, int obj, V3 o, V
             h.N = {f1.x, f1.y, f1.z};
         }
     } else {
-        float4 s = p.sscan[obj - p.nf];
+        float4 s = row(p.sscan, obj - p.nf);
         h.N = vnorm(vdiv(vsub(h.P, V3{s.x, s.y, s.z}), s.w));
     }
     return h;
@@ -870,7 +891,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
     const HitRec hr = hit_geometry(p, obj, o, d, t);
     const V3 P = hr.P;
     V3 N = hr.N;
-    const ObjK &ob = p.objs[obj];
+    const ObjK &ob = row(p.objs, obj);
     V3 I = vmul(d, -1.0f);
     float cosI = vdot(N, I);
     C3 dif = {ob.dif[0], ob.dif[1], ob.dif[2]};
@@ -889,7 +910,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
                                 (float)((double)width - 1.0));
             dif = {texel(p, tx, j, i, 0), texel(p, tx, j, i, 1), texel(p, tx, j, i, 2)};
         } else {                                                     // main.cpp:834-861
-            const FaceShadeK &fs = p.fsh[obj];
+            const FaceShadeK &fs = row(p.fsh, obj);
             float u = (hr.ba * fs.vt[0][0]) + (hr.bb * fs.vt[1][0]) + (hr.bg * fs.vt[2][0]);
             float v = (hr.ba * fs.vt[0][1]) + (hr.bb * fs.vt[1][1]) + (hr.bg * fs.vt[2][1]);
             v = clampr(v, 0.0f, 1.0f);
@@ -923,18 +944,18 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
     copy_stack(f, fc, c, root);
     int n = fsn;
     Medium m;
-    float hit_eta = p.objs[hit].eta;
+    float hit_eta = row(p.objs, hit).eta;
     if (h_state(f) == ENTERING) {
         if (hit == f.obj) {
             m.state = EXITING;
             if (n > 0) {
-                m.ei = p.objs[c.stack[n - 1]].eta;
+                m.ei = row(p.objs, c.stack[n - 1]).eta;
                 n--;
             } else {
                 m.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
                 cnt.ub++;
             }
-            m.et = n > 0 ? p.objs[c.stack[n - 1]].eta : p.eta_bkg;
+            m.et = n > 0 ? row(p.objs, c.stack[n - 1]).eta : p.eta_bkg;
             if (n > 0) n--;
         } else {
             m.state = ENTERING;
@@ -951,7 +972,7 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
         } else {
             m.state = EXITING;
             m.ei = f.et;
-            m.et = p.objs[c.stack[n - 1]].eta;
+            m.et = row(p.objs, c.stack[n - 1]).eta;
             n--;
         }
     } else {
@@ -973,7 +994,7 @@ __device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAX
     copy_stack(f, fc, c, root);
     int n = fsn;
     Medium m;
-    float hit_eta = p.objs[hit].eta;
+    float hit_eta = row(p.objs, hit).eta;
     if (h_state(f) == ENTERING) {
         m.state = ENTERING;
         m.ei = f.ei;
@@ -982,7 +1003,7 @@ __device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAX
                 m.et = hit_eta;
                 c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
             } else {
-                m.et = p.objs[c.stack[n - 1]].eta;
+                m.et = row(p.objs, c.stack[n - 1]).eta;
                 n--;
             }
         } else {
@@ -1070,7 +1091,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             color = bkg;
             return RK_NONE;
         }
-        m = Medium{ENTERING, 1, p.eta_bkg, p.objs[q.win].eta};   // stack {q.win}: implicit (copy_stack)
+        m = Medium{ENTERING, 1, p.eta_bkg, row(p.objs, q.win).eta};   // stack {q.win}: implicit (copy_stack)
         open = true;
         top = 0;
     } else {
@@ -1085,7 +1106,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             // that ray's direction for a point light, the constant -L for a
             // directional one (q.d is not modified by a trace)
             V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
-            const ObjK &ob = p.objs[h.obj];
+            const ObjK &ob = row(p.objs, h.obj);
             // H only feeds the specular power: rsqrt instead of 3 IEEE
             // divisions (<= 2 ulp; vnorm(0) = NaN either way)
             V3 hv = vadd(L, h.I);
@@ -1117,8 +1138,8 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 set_phase(h, PH_REFR_CHILD);
                 open = true;
             } else {
-                const ObjK &ob = p.objs[h.obj];
-                C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)h.dif.r)), (float)(1.0 - (double)ob.opacity));
+                C3 tr = cmulf(cmulf(bkg, (float)(1.0 - (double)h.dif.r)),
+                              (float)(1.0 - (double)row(p.objs, h.obj).opacity));
                 h.acc = cadd(h.acc, tr);
                 set_phase(h, PH_REFL);
             }
@@ -1129,7 +1150,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 open = true;
             } else {
                 // miss: refl = bkg * F_r; finish this node below
-                h.acc = cadd(h.acc, cmulf(bkg, refl_fresnel(p.objs[h.obj], cos_i(h))));
+                h.acc = cadd(h.acc, cmulf(bkg, refl_fresnel(row(p.objs, h.obj), cos_i(h))));
                 set_phase(h, PH_DONE);
             }
         }
@@ -1150,8 +1171,8 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
     }
     // ---- run the top node forward (phase PH_LIGHT here: its last light is done) ----
     for (;;) {
-        const ObjK &ob = p.objs[h.obj];
         if (h_phase(h) == PH_LIGHT) {
+            const ObjK &ob = row(p.objs, h.obj);
             // ambient + specular sum, then Fresnel / transmission (main.cpp:961-992)
             h.acc = cadd(cmulf(h.dif, ob.ka), h.acc);
             const float cosI = cos_i(h);
@@ -1176,6 +1197,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             set_phase(h, PH_REFL);
         }
         if (h_phase(h) == PH_REFL) {                 // main.cpp:1103-1124
+            const ObjK &ob = row(p.objs, h.obj);
             const float cosI = cos_i(h);
             float Fr = refl_fresnel(ob, cosI);
             if (p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
@@ -1196,7 +1218,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         }
         top--;
         q.o = cold_restore(ls.cold()[top], h);
-        const ObjK &pob = p.objs[h.obj];
+        const ObjK &pob = row(p.objs, h.obj);
         if (h_phase(h) == PH_REFR_CHILD) {           // main.cpp:1072-1083
             C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)h.dif.r)), (float)(1.0 - (double)pob.opacity));
             h.acc = cadd(h.acc, tr);
