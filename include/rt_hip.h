@@ -203,9 +203,9 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * stream by events: renders issued on different caller streams -- independent
  * frames -- overlap, so one frame's tail is filled by the next frame's work),
  * "lds_stack" (12..16, default 14: BVH stack entries kept in LDS per lane;
- * deeper stacks spill to device memory -- a test knob), "bvh_leaf",
- * "bvh_trav" (binary SAH: largest leaf, node cost x1000), "bvh_collapse"
- * (0 greedy, 1 SAH-optimal 4-wide collapse), "bvh_node" (its node cost x1000),
+ * deeper stacks spill to device memory -- a test knob), "bvh_leaf" (largest
+ * leaf), "bvh_collapse" (0 greedy, 1 SAH-optimal 4-wide collapse), "bvh_node"
+ * (the collapse's node cost x1000),
  * "chunk" (0..4096: pixels a wave takes from the work counter at a time,
  * 0 = as many as it has idle lanes; default: 64, one 8x8 tile, when some
  * material reflects or refracts, else 0 -- never changes the image),

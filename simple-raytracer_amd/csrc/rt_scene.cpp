@@ -67,7 +67,6 @@ struct rt_scene {
     long long opt_reserve = 0;         // occupancy-derived grid: block slots left free for other kernels
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
     long long opt_bvh_leaf = 8;        // SAH max leaf size
-    long long opt_bvh_trav = 500;      // SAH traversal cost, x1000 of a sphere test (A/B: 0.5 best)
     long long opt_bvh_collapse = 1;    // binary -> 4-wide: 0 greedy (largest area first), 1 SAH-optimal DP
     long long opt_bvh_node = 500;      // DP collapse: cost of a 4-wide node visit, x1000 of a sphere test
                                        // (A/B, C3: 0.25 / 0.5 / 0.75 / 1 / 2 -> +0.6 / +0.5 / +0.5 / +0.2 / -1.7 %)
@@ -224,7 +223,7 @@ double distance_bound(const rt_scene *s, const float eye[3]) {
 bool build_wide(rt_scene *s, std::vector<rtbvh::Prim> &P, rtbvh::Result &R, rtbvh::Result4 &Q) {
     rtbvh::Builder B(P);
     B.max_leaf = s->opt_bvh_collapse ? 1 : (int)s->opt_bvh_leaf;
-    B.trav_cost = (float)s->opt_bvh_trav / 1000.0f;
+    B.trav_cost = 0.5f;                // SAH node cost, in sphere tests (A/B over 0.25-2: 0.5 best, round 1)
     if (!B.build(R) || R.nodes.empty()) return false;
     if (s->opt_bvh_collapse)
         rtbvh::collapse_sah<4>(R, Q, (int)s->opt_bvh_leaf, (float)s->opt_bvh_node / 1000.0f);
@@ -904,9 +903,8 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         if (value < kSpill + 4 || value > kLdsStack) return RT_E_INVALID;
         s->opt_lds_stack = value;
     }
-    else if (k == "bvh_leaf" || k == "bvh_trav" || k == "bvh_collapse" || k == "bvh_node") {
+    else if (k == "bvh_leaf" || k == "bvh_collapse" || k == "bvh_node") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
-        else if (k == "bvh_trav") s->opt_bvh_trav = std::max(0LL, value);
         else if (k == "bvh_collapse") s->opt_bvh_collapse = value != 0;
         else s->opt_bvh_node = std::max(0LL, value);
         s->bvh_D = -1.0;               // rebuild on the next render
