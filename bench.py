@@ -63,7 +63,8 @@ def parse_args():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: step k renders on stream k mod F (rt_scene option "
                          "'inflight'), so one frame's tail overlaps the next frame's work; "
-                         "0 = 2 at N=1, 4 at N>1 (a frame never waits for the gather two frames back; an even count keeps consecutive frames on different hardware queues)")
+                         "0 = 2 at N=1 (3 or 4: no gain), 8 at N>1 (a rank's short frame leaves a long tail: "
+                         "8 in flight take C3's N=8 share from 2.36 to 2.25 ms, profiles/r03/inflight_n8.txt)")
     ap.add_argument("--reserve", type=int, default=-1,
                     help="block slots the persistent render leaves free (rt_scene option 'reserve'); "
                          "-1 = 0 at N=1, 8 at N>1 (room for the RCCL gather beside the next frame)")
@@ -201,7 +202,7 @@ def main() -> None:
     # F frames in flight: frame k renders into buffer k mod F, ordered on
     # stream k mod F (the render on a library stream of its own, the gather
     # after it); frame k+1 on the next stream overlaps frame k's tail.
-    F = max(1, min(4, args.inflight if args.inflight > 0 else (2 if world == 1 else 4)))
+    F = max(1, min(8, args.inflight if args.inflight > 0 else (2 if world == 1 else 8)))
     reserve = args.reserve if args.reserve >= 0 else (0 if world == 1 else 8)
     if reserve:
         gs.set_option("reserve", reserve)

@@ -197,7 +197,7 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * (persistent blocks, 0 = occupancy), "reserve" (block slots the occupancy-
  * sized grid leaves free, e.g. for a collective's kernel that must run beside
  * a persistent render), "depth" (recursion depth override),
- * "inflight" (1..4, default 1: renders of this scene that may run at once.
+ * "inflight" (1..8, default 1: renders of this scene that may run at once.
  * With n > 1 each render gets its own work counter, counters and ShadeRay
  * frame buffer and runs on a library stream, ordered against its caller's
  * stream by events: renders issued on different caller streams -- independent

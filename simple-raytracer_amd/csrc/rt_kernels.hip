@@ -1332,10 +1332,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             kind = advance<MAXF>(p, ls, q, cnt, color);
             pending = kind != RK_NONE;
             if (!pending) {
-                float *o = p.out + ((size_t)py * p.W + px) * 3;
-                o[0] = color.r;
-                o[1] = color.g;
-                o[2] = color.b;
+                // the pixel's 12 bytes in one store (global_store_dwordx3)
+                typedef float f3v __attribute__((ext_vector_type(3), aligned(4)));
+                *reinterpret_cast<f3v *>(p.out + ((size_t)py * p.W + px) * 3) = f3v{color.r, color.g, color.b};
                 busy = false;
             }
         }

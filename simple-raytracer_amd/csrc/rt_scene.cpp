@@ -577,7 +577,7 @@ int init_slot(RenderSlot &r, bool own_stream) {
 }
 
 int set_inflight(rt_scene *s, long long n) {
-    if (n < 1 || n > 4) return RT_E_INVALID;
+    if (n < 1 || n > 8) return RT_E_INVALID;
     if ((size_t)n == s->slots.size()) return RT_OK;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     for (auto &r : s->slots) free_slot(r);

@@ -395,7 +395,7 @@ def test_frames_in_flight(inflight):
     img, _ = gs.render_rows(cam, W, H, 0, H)
     assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9))
     with pytest.raises(rtamd.RTError):
-        gs.set_option("inflight", 5)
+        gs.set_option("inflight", 9)
 
 
 def test_abi_errors():

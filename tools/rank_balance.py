@@ -8,7 +8,7 @@ the ranks do not slow each other down (each has its own GPU) and adds the
 RCCL gather's xGMI time estimate (strip bytes / 153 GB/s per link, SURVEY.md
 §8e).  PROJECTED, not measured on N GPUs.
 
-  python tools/rank_balance.py C3 [--frames 8] [--inflight 4] [--reserve 8]
+  python tools/rank_balance.py C3 [--frames 8] [--inflight 8] [--reserve 8]
 """
 from __future__ import annotations
 
@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config", nargs="?", default="C3")
     ap.add_argument("--frames", type=int, default=8)
-    ap.add_argument("--inflight", type=int, default=4)
+    ap.add_argument("--inflight", type=int, default=8)
     ap.add_argument("--reserve", type=int, default=8)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--option", action="append", default=[], help="kernel option key=value (both scenes)")
