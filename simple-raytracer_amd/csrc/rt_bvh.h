@@ -307,10 +307,11 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
 
 // Device form of a 4-wide node (80 B, 5 x 16 B; after Ylitie et al. 2017,
 // with half-precision instead of 8-bit plane offsets): the node's box origin,
-// one power-of-two scale 2^e per axis, each child's bounds as binary16
-// multiples h of it -- lower bounds rounded down, upper bounds rounded up, to
-// the binary16 grid (child i in half i % 2 of word i / 2) -- then the links.
-// Child box on axis a: [origin_a + hlo * 2^e_a, origin_a + hhi * 2^e_a]; it
+// one power-of-two scale 2^e for the three axes (stored as the float 2^e: the
+// device forms 2^e / d with one multiply per axis), each child's bounds as
+// binary16 multiples h of it -- lower bounds rounded down, upper bounds rounded
+// up, to the binary16 grid (child i in half i % 2 of word i / 2) -- then the
+// links.  Child box on axis a: [origin_a + hlo * 2^e, origin_a + hhi * 2^e]; it
 // contains the float box exactly (real arithmetic), and the device's
 // slab-test rounding is of the order of ulp(D), far inside the primitives'
 // padding (rt_kernels.hip).  The device converts h inside the plane FMA
@@ -318,7 +319,7 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
 // relative resolution (8-bit offsets: 1/255) -- tighter boxes.
 struct Node4H {
     float origin[3];
-    int8_t exp[4];           // exponents e of the x, y, z scales 2^e (-126 <= e <= kQExpMax); [3] unused
+    float scale;             // 2^e (-126 <= e <= kQExpMax), one for the three axes
     uint32_t lo[3][2];       // per axis: lower bounds of children (0, 1), (2, 3)
     uint32_t hi[3][2];       // per axis: upper bounds
     int32_t link[4];
@@ -366,34 +367,38 @@ inline bool quantize(const Result4 &Q, std::vector<Node4H> &out) {
         const Node4 &n = Q.nodes[k];
         Node4H &z = out[k];
         for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
-        z.exp[3] = 0;
+        double lo[3], hi[3];
+        int e = -126;
         for (int a = 0; a < 3; a++) {
             auto empty = [&](int i) {              // no slot, or an empty leaf (inverted box)
                 return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]);
             };
-            double lo = INFINITY, hi = -INFINITY;
+            lo[a] = INFINITY, hi[a] = -INFINITY;
             for (int i = 0; i < 4; i++) {
                 if (empty(i)) continue;
                 if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
-                lo = std::min(lo, (double)n.lo[a][i]);
-                hi = std::max(hi, (double)n.hi[a][i]);
+                lo[a] = std::min(lo[a], (double)n.lo[a][i]);
+                hi[a] = std::max(hi[a], (double)n.hi[a][i]);
             }
-            if (!(lo <= hi)) lo = hi = 0.0;              // no child at all
-            z.origin[a] = (float)lo;                     // exact: lo is a float
-            // smallest scale 2^e with kHMax * 2^e >= extent (normal floats only)
-            double ext = hi - lo;
-            int e = -126;
-            while (e < 127 && std::ldexp(kHMax, e) < ext) e++;
-            if (e > kQExpMax) return false;
-            z.exp[a] = (int8_t)e;
-            double sc = std::ldexp(1.0, e);
+            if (!(lo[a] <= hi[a])) lo[a] = hi[a] = 0.0;  // no child at all
+            z.origin[a] = (float)lo[a];                  // exact: lo is a float
+            // smallest scale 2^e with kHMax * 2^e >= every axis' extent (normal
+            // floats only); binary16 is floating point, so a shorter axis keeps
+            // 11 significant bits in its offsets
+            while (e < 127 && std::ldexp(kHMax, e) < hi[a] - lo[a]) e++;
+        }
+        if (e > kQExpMax) return false;
+        const double sc = std::ldexp(1.0, e);
+        z.scale = (float)sc;                             // exact: a normal power of two
+        for (int a = 0; a < 3; a++) {
+            auto empty = [&](int i) { return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]); };
             z.lo[a][0] = z.lo[a][1] = z.hi[a][0] = z.hi[a][1] = 0;
             for (int i = 0; i < 4; i++) {
                 uint32_t l = kHalfHMax, h = 0;           // empty slot: inverted box
                 if (!empty(i)) {
                     // exact in double: float differences, power-of-two scale
-                    l = half_round(std::min(kHMax, ((double)n.lo[a][i] - lo) / sc), false);
-                    h = half_round(std::min(kHMax, ((double)n.hi[a][i] - lo) / sc), true);
+                    l = half_round(std::min(kHMax, ((double)n.lo[a][i] - lo[a]) / sc), false);
+                    h = half_round(std::min(kHMax, ((double)n.hi[a][i] - lo[a]) / sc), true);
                 }
                 z.lo[a][i / 2] |= l << (16 * (i % 2));
                 z.hi[a][i / 2] |= h << (16 * (i % 2));

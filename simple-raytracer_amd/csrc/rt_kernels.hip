@@ -332,11 +332,11 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 }
 
 // The six plane distances of a 4-wide node's children (rt_bvh.h Node4H):
-// plane a of child i at origin_a + h * 2^e_a (h binary16), i.e.
-// t = h * (2^e_a / d_a) + (origin_a - o_a) / d_a = fma(h, A_a, B_a) -- one
-// v_fma_mix_f32 per plane (h converted inside the fma, exactly); the rounding
-// (~ulp(D) in distance) is far inside the primitive padding.  (i, o) =
-// (1 / d, o / d) per axis, or (1, o) for a point query: then the planes are
+// plane a of child i at origin_a + h * 2^e (h binary16, one scale 2^e per
+// node), i.e. t = h * (2^e / d_a) + (origin_a - o_a) / d_a = fma(h, A_a, B_a)
+// -- one v_fma_mix_f32 per plane (h converted inside the fma, exactly); the
+// rounding (~ulp(D) in distance) is far inside the primitive padding.  (i, o)
+// = (1 / d, o / d) per axis, or (1, o) for a point query: then the planes are
 // the children's offsets from o.  Near / far plane per axis by the ray's
 // octant: t(h) is monotonic in h with the sign of A (= the sign of 1/d), so
 // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10.
@@ -346,12 +346,9 @@ struct ChildPlanes {
 __device__ __forceinline__ ChildPlanes child_planes(float4 w0, float4 w1, float4 w2, float4 w3, float ix, float iy,
                                                     float iz, float ox, float oy, float oz, bool neg_x, bool neg_y,
                                                     bool neg_z) {
-    // 2^e * (1/d): exact power-of-two scaling (one v_bfe_i32 + v_ldexp per
-    // axis; signed exponents in bytes 0..2 of w0.w), finite by the caps
-    const int ex = __float_as_int(w0.w);
-    const float A[3] = {__builtin_amdgcn_ldexpf(ix, __builtin_amdgcn_sbfe(ex, 0, 8)),
-                        __builtin_amdgcn_ldexpf(iy, __builtin_amdgcn_sbfe(ex, 8, 8)),
-                        __builtin_amdgcn_ldexpf(iz, __builtin_amdgcn_sbfe(ex, 16, 8))};
+    // 2^e * (1/d): an exact power-of-two scaling (w0.w = 2^e), finite by the
+    // caps (|1/d| <= 2^100, e <= kQExpMax)
+    const float A[3] = {ix * w0.w, iy * w0.w, iz * w0.w};
     const float B[3] = {fmaf(w0.x, ix, -ox), fmaf(w0.y, iy, -oy), fmaf(w0.z, iz, -oz)};
     // lower / upper bounds per axis, two children per word
     const unsigned lo[3][2] = {{__float_as_uint(w1.x), __float_as_uint(w1.y)},
@@ -378,13 +375,25 @@ __device__ __forceinline__ ChildPlanes child_planes(float4 w0, float4 w1, float4
     return cp;
 }
 
-// Entry distance of a ray into child i within [tlo, thi]: +inf for a miss or
+// Sort key of a child: the bits of its entry distance, kMissKey for a miss or
 // an empty slot (unused slots link to the empty leaf, kEmptyLeaf: entering one
-// is harmless, so no link test; their inverted boxes miss anyway).
-__device__ __forceinline__ float child_entry(const ChildPlanes &cp, int i, float tlo, float thi) {
-    const float tn = fmaxf(fmaxf(cp.tn[0][i], cp.tn[1][i]), fmaxf(cp.tn[2][i], tlo));
-    const float tf = fminf(fminf(cp.tf[0][i], cp.tf[1][i]), fminf(cp.tf[2][i], thi));
-    return (tn <= tf) ? tn : kInf;
+// is harmless, so no link test; their inverted boxes miss anyway).  The entry
+// distance is >= tlo >= 0 whenever tmin >= 0, and for non-negative floats the
+// unsigned order is the float order; otherwise only the visiting order (speed)
+// changes.  kMissKey (-1) is an inline constant, +inf as a float is not (one
+// v_mov per node visit); as a float it is a NaN, which tn <= tf excludes.
+constexpr unsigned kMissKey = ~0u;
+//
+// tlo / thi join through the NaN-propagating maximum / minimum (gfx950
+// v_maximum3_f32 / v_minimum3_f32), which need no canonicalised operands:
+// with fmaxf / fminf the compiler canonicalises the two loop-carried bounds in
+// every node visit.  A plane is NaN only if fma(h, A, B) meets inf - inf
+// (coordinates beyond ~2^26 with a capped 1/d); the outer fmaxf / fminf then
+// drop the bound together with it -- a wider interval, still conservative.
+__device__ __forceinline__ unsigned child_entry(const ChildPlanes &cp, int i, float tlo, float thi) {
+    const float tn = fmaxf(fmaxf(cp.tn[0][i], cp.tn[1][i]), __builtin_elementwise_maximum(cp.tn[2][i], tlo));
+    const float tf = fminf(fminf(cp.tf[0][i], cp.tf[1][i]), __builtin_elementwise_minimum(cp.tf[2][i], thi));
+    return (tn <= tf) ? __float_as_uint(tn) : kMissKey;
 }
 
 // stk: this lane's traversal stack in LDS (entries kBlock apart).
@@ -439,8 +448,11 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     int sp = 1;
     int node = rtbvh::kEmpty;                  // >= 0 inner node, < 0 leaf, kEmpty: done
     int leaf = rtbvh::kEmpty;                  // postponed leaf
+    // the culling bound, widened by 2^-16: one multiply of the selected bound
+    // (x * (1 + 2^-16) rounds the real x + x 2^-16 once, as x + x * 2^-16
+    // does: the same bound, one instruction fewer)
     auto thi_now = [&] {
-        return point ? 0.0f : q.closest ? best + best * 0x1p-16f : (q.unb ? kInf : q.tmax + q.tmax * 0x1p-16f);
+        return point ? 0.0f : (q.closest ? best : (q.unb ? kInf : q.tmax)) * (1.0f + 0x1p-16f);
     };
     // LDS holds stack entries [0, kLdsStack); entry 0 is kEmpty, or kRefill + b
     // when b blocks of kSpill older entries wait in device memory (ovf).
@@ -480,7 +492,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         float thi = thi_now();
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
         const ChildPlanes cp = child_planes(w0, w1, w2, w3, ix, iy, iz, ox, oy, oz, neg_x, neg_y, neg_z);
-        float k[4];
+        unsigned k[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             if (!point) {
@@ -496,17 +508,17 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
                 float dx = fmaxf(fmaxf(tnx, -tfx), 0.0f), dy = fmaxf(fmaxf(tny, -tfy), 0.0f);
                 float d2 = fmaf(dx, dx, dy * dy);
                 bool in = (tfz >= 0.0f) & (d2 <= cone_k * (tfz * tfz)) & (tnz <= cone_h);
-                k[i] = in ? d2 : kInf;           // nearest the cone's axis first
+                k[i] = in ? __float_as_uint(d2) : kMissKey;   // nearest the cone's axis first (d2 >= 0)
             }
         }
         // up to 3 pushes below write stk[sp .. sp + 2]: make room (rare)
         if (sp > p.stack_cap - 3) spill();
-        float k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
+        unsigned k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3];
         // nearest child by a 3-comparator tournament, registers only
 #define RT_CSWAP(ka, ca, kb, cb)                 \
     {                                            \
         bool sw = kb < ka;                       \
-        float tk = sw ? kb : ka;                 \
+        unsigned tk = sw ? kb : ka;              \
         kb = sw ? ka : kb;                       \
         ka = tk;                                 \
         int tc = sw ? cb : ca;                   \
@@ -523,12 +535,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         // losers c1, c3 below it -- the visiting order only affects speed,
         // every hit child is visited
         stk[sp * kBlock] = c3;
-        sp += k3 < kInf ? 1 : 0;
+        sp += k3 != kMissKey ? 1 : 0;
         stk[sp * kBlock] = c1;
-        sp += k1 < kInf ? 1 : 0;
+        sp += k1 != kMissKey ? 1 : 0;
         stk[sp * kBlock] = c2;
-        sp += k2 < kInf ? 1 : 0;
-        if (k0 < kInf) {
+        sp += k2 != kMissKey ? 1 : 0;
+        if (k0 != kMissKey) {
             node = c0;
         } else {
             node = pop();

@@ -134,7 +134,7 @@ static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int
         if (!quantize(Q4, QQ)) { printf("FAIL quantize4\n"); return 1; }
         for (size_t k = 0; k < Q.nodes.size(); k++)
             for (int a = 0; a < 3; a++) {
-                double sc = std::ldexp(1.0, (int)QQ[k].exp[a]), o = QQ[k].origin[a];
+                double sc = (double)QQ[k].scale, o = QQ[k].origin[a];
                 for (int i = 0; i < 4; i++) {
                     double l = half_value((QQ[k].lo[a][i / 2] >> (16 * (i % 2))) & 0xffff);
                     double h = half_value((QQ[k].hi[a][i / 2] >> (16 * (i % 2))) & 0xffff);
