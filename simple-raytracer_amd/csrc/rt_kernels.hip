@@ -129,7 +129,13 @@ __device__ __forceinline__ bool face_test(float4 f0, float4 f1, float4 f2, float
     b = (d22 * d1p - d12 * d2p) / det;
     g = (d11 * d2p - d12 * d1p) / det;
     a = 1.0f - (b + g);
-    return (dem != 0.0f) & (0.0f < a) & (a < 1.0f) & (0.0f < b) & (b < 1.0f) & (0.0f < g) & (g < 1.0f);
+    // 0 < a, b, g < 1 as two compares of the NaN-propagating minimum / maximum
+    // (gfx950 v_minimum3_f32 / v_maximum3_f32): a NaN fails both, as it fails
+    // every one of the six compares; six compares joined by & were lowered to
+    // ~20 bit operations on bytes
+    const float mn = __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), g);
+    const float mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), g);
+    return (dem != 0.0f) && (mn > 0.0f) && (mx < 1.0f);
 }
 
 // TraceRay's sphere test (main.cpp:1225-1258): both roots, A = 1 assumed.
@@ -275,8 +281,8 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
     int nfc = (v >> 4) & 15, count = v & 15;
     if (faces_only) count = nfc;             // the leaf's faces come first
     for (int k = 0; k < count; k++) {
-        float t[2];
-        int nt = 0;
+        float t0 = 0.0f, t1 = 0.0f;          // candidate roots: a face has one (h0), a sphere two (h0, h1)
+        bool h0, h1;
         int key;
         float fac;
         // one batch of loads for either kind; the face words 2..4 only when
@@ -296,35 +302,46 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
             fac = f4.z;
             float a, bb, g;
             RT_COUNT(cnt.ftests++);
-            if (face_test(f0, f1, f2, f3, f4, q.o, q.d, t[0], a, bb, g) & (f1.w != 0.0f)) nt = 1;
+            h0 = face_test(f0, f1, f2, f3, f4, q.o, q.d, t0, a, bb, g) && (f1.w != 0.0f);
+            h1 = false;
         } else {
             R += 2;
             key = __float_as_int(f1.x);
             fac = f1.y;
             RT_COUNT(cnt.stests++);
-            if (sphere_test(f0, q.o, q.d, t[0], t[1])) nt = 2;
+            h0 = h1 = sphere_test(f0, q.o, q.d, t0, t1);
         }
-        for (int r = 0; r < nt; r++) {
-            float tt = t[r];
-            if (q.closest) {
-                bool valid = (tt > q.tmin) & (tt < kFltMax);
-                bool better = (tt < best) | ((tt == best) & (key < win));
+        // the roots in order, straight-line (a loop over them cost a select,
+        // a counter and a branch per root)
+        if (q.closest) {
+            auto take = [&](float tt, bool h) {
+                const bool valid = h & (tt > q.tmin) & (tt < kFltMax);
+                const bool better = (tt < best) | ((tt == best) & (key < win));
                 if (valid & better) {
                     best = tt;
                     win = key;
                 }
-            } else if (q.skipchk) {
-                // SKIP_TRANS (main.cpp:997-1002): a candidate of another
-                // object that the reference's in-order scan would see as a
-                // new minimum -- any one before the stack top's object in
-                // order, or nearer than the stack top's own nearest root
-                // (q.tmax) -- aborts the refraction
-                if ((key != q.back) & (tt > q.tmin) & (tt < kFltMax) & ((key < q.back) | (tt < q.tmax))) opaque = true;
-            } else if ((key != q.self) & (tt > q.tmin) & ((tt < q.tmax) | q.unb)) {
+            };
+            take(t0, h0);
+            take(t1, h1);
+        } else if (q.skipchk) {
+            // SKIP_TRANS (main.cpp:997-1002): a candidate of another object
+            // that the reference's in-order scan would see as a new minimum --
+            // any one before the stack top's object in order, or nearer than
+            // the stack top's own nearest root (q.tmax) -- aborts the refraction
+            auto aborts = [&](float tt, bool h) {
+                return h & (tt > q.tmin) & (tt < kFltMax) & ((key < q.back) | (tt < q.tmax));
+            };
+            if ((key != q.back) & (aborts(t0, h0) | aborts(t1, h1))) opaque = true;
+        } else if (key != q.self) {
+            auto shadows = [&](float tt, bool h) { return h & (tt > q.tmin) & ((tt < q.tmax) | q.unb); };
+            const bool s0 = shadows(t0, h0), s1 = shadows(t1, h1);
+            if (s0 || s1) {
                 if (fac == 0.0f && p.shadow_early_out) {
                     opaque = true;
                 } else if (!PRE) {
-                    q.mask = cmulf(q.mask, fac);
+                    if (s0) q.mask = cmulf(q.mask, fac);
+                    if (s1) q.mask = cmulf(q.mask, fac);
                 }
             }
         }
