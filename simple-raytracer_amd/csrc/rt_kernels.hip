@@ -281,7 +281,8 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
     int nfc = (v >> 4) & 15, count = v & 15;
     if (faces_only) count = nfc;             // the leaf's faces come first
     for (int k = 0; k < count; k++) {
-        float t0 = 0.0f, t1 = 0.0f;          // candidate roots: a face has one (h0), a sphere two (h0, h1)
+        float t0, t1;                        // candidate roots: a face has one (h0), a sphere two (h0, h1);
+                                             // a root is read only under its flag
         bool h0, h1;
         int key;
         float fac;
@@ -289,9 +290,15 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
         // some lane of the wave is at a face (a sphere then reads 3 words past
         // its record; the stream is padded for the last one) -- the vector
         // memory path (TA), not the ALU, is the busier one here
+        // (w2..w4 are not zeroed when no lane is at a face: only the face
+        // branch reads them, and no lane takes it then -- 12 v_mov per leaf
+        // primitive saved)
         const f4v *RV = reinterpret_cast<const f4v *>(R);
-        f4v w0 = RV[0], w1 = RV[1], w2 = {0.0f, 0.0f, 0.0f, 0.0f}, w3 = w2, w4 = w2;
-        if (__ballot(k < nfc)) w2 = RV[2], w3 = RV[3], w4 = RV[4];
+        f4v w0 = RV[0], w1 = RV[1], w2, w3, w4;
+        if (__ballot(k < nfc))
+            w2 = RV[2], w3 = RV[3], w4 = RV[4];
+        else                                 // whatever the registers hold: no instruction
+            asm("" : "=v"(w2), "=v"(w3), "=v"(w4));
         asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
         float4 f0 = make_float4(w0.x, w0.y, w0.z, w0.w), f1 = make_float4(w1.x, w1.y, w1.z, w1.w);
         float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
@@ -486,8 +493,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         stk[0] = kRefill + nb + 1;
         atomicAdd(&p.stats[34], 1ull);
     };
-    auto pop = [&]() -> int {
-        int n = stk[(--sp) * kBlock];
+    // pop the top entry, whose value n the caller has already read (stk[sp - 1])
+    auto pop_value = [&](int n) -> int {
+        --sp;
         if ((unsigned)n - (unsigned)kRefill - 1u < (unsigned)(kStackMax / kSpill)) {   // rare: bring a block back
             const int nb = n - kRefill;
             const int *o = ovf_lane() + (nb - 1) * kSpill;
@@ -498,6 +506,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         }
         return n;
     };
+    auto pop = [&]() -> int { return pop_value(stk[(sp - 1) * kBlock]); };
     // One 4-wide node (rt_bvh.h Node4H, child_planes): slab-test the
     // children, push the far hits, continue with the nearest, park the first
     // leaf reached.
@@ -506,6 +515,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         cnt.trips++;
 #endif
         RT_COUNT(cnt.boxes += 4);
+        // the stack top, read while the node's planes are computed: a pop at
+        // the end of the visit then waits for no LDS read before the next
+        // node fetch (spill() below moves entries, not the top's value)
+        const int top0 = stk[(sp - 1) * kBlock];
         float thi = thi_now();
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
         const ChildPlanes cp = child_planes(w0, w1, w2, w3, ix, iy, iz, ox, oy, oz, neg_x, neg_y, neg_z);
@@ -557,14 +570,16 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         sp += k1 != kMissKey ? 1 : 0;
         stk[sp * kBlock] = c2;
         sp += k2 != kMissKey ? 1 : 0;
+        // the top after the pushes, from registers
+        const int top1 = k2 != kMissKey ? c2 : k1 != kMissKey ? c1 : k3 != kMissKey ? c3 : top0;
         if (k0 != kMissKey) {
             node = c0;
         } else {
-            node = pop();
+            node = pop_value(top0);            // no child hit: nothing was pushed
         }
         if (node < 0 && node != rtbvh::kEmpty && leaf == rtbvh::kEmpty) {
             leaf = node;                       // park it, keep descending
-            node = pop();
+            node = k0 != kMissKey ? pop_value(top1) : pop();
         }
     };
     // The root (every trace starts there; wave-uniform) comes through scalar
