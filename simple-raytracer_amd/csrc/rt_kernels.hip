@@ -1219,14 +1219,23 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             const ObjK &ob = row(p.objs, h.obj);
             // ambient + specular sum, then Fresnel / transmission (main.cpp:961-992)
             h.acc = cadd(cmulf(h.dif, ob.ka), h.acc);
-            const float cosI = cos_i(h);
-            float snell = h.ei / h.et;
-            float crit = asinf(h.et / h.ei);
-            float inc = acosf(cosI);
-            bool tir = (crit < inc) && ((double)inc < kRightAngle);
-            float F0 = (h.et - h.ei) / (h.et + h.ei);
-            h.dif.r = schlick(F0 * F0, cosI);        // F_t (the diffuse colour is no longer needed)
-            if (p.depth - top > 0 && !tir && (double)ob.opacity < 1.0 && ob.eta > 0) {
+            // TIR, F_t and the refraction direction only for a node that can
+            // refract: the reference computes them for every node
+            // (main.cpp:961-992), but they feed nothing else, and a wave with
+            // no such lane then skips the asinf / acosf / double Schlick code
+            bool refr = p.depth - top > 0 && (double)ob.opacity < 1.0 && ob.eta > 0;
+            float cosI = 0.0f, snell = 0.0f;
+            if (refr) {
+                cosI = cos_i(h);
+                snell = h.ei / h.et;
+                float crit = asinf(h.et / h.ei);
+                float inc = acosf(cosI);
+                bool tir = (crit < inc) && ((double)inc < kRightAngle);
+                float F0 = (h.et - h.ei) / (h.et + h.ei);
+                h.dif.r = schlick(F0 * F0, cosI);    // F_t (the diffuse colour is no longer needed)
+                refr = !tir;
+            }
+            if (refr) {
                 float k = sqrtf((float)(1.0 - (double)(snell * snell) * (1.0 - (double)(cosI * cosI))));
                 V3 T = vadd(vmul(vmul(h.N, -1.0f), k), vmul(vsub(vmul(h.N, cosI), h.I), snell));
                 closest_query(q, p, T, h.obj);
