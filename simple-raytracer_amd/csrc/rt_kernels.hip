@@ -246,6 +246,17 @@ __device__ __forceinline__ float own_nearest(const Query &q, const Params &p, in
 }
 
 
+// Raw buffer resource over a device array (gfx9 dword3: 32-bit data format;
+// the range is not used for bounds: every offset the kernel forms is in range)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+// 16 bytes at byte offset off + imm (imm a constant: the instruction's offset field)
+__device__ __forceinline__ f4v bldv(__amdgpu_buffer_rsrc_t r, int off, int imm) {
+    return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off + imm, 0, 0));
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int off, int imm) { return f4(bldv(r, off, imm)); }
+
 constexpr int kNodeF4 = 5;                       // float4 per 4-wide node (rt_bvh.h Node4H)
 static_assert(kNodeF4 * 16 == sizeof(rtbvh::Node4H), "node layout");
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plane offsets
@@ -253,17 +264,26 @@ typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plan
 // look for a leaf (A/B, C3 Mrays/s: 0 -> 5912, 1 -> 5960, 2 -> 5957, 3 -> 5954,
 // 6 -> 5924, 12 -> 5849; with one leaf per round: 0 -> 5885, 2 -> 6021,
 // 5 -> 6031; profiles/r02/ab_leaf_*.txt)
-constexpr unsigned kLeafWait = 2;
+#ifndef RT_LEAF_WAIT
+#define RT_LEAF_WAIT 2
+#endif
+constexpr unsigned kLeafWait = RT_LEAF_WAIT;
 // The depth > 4 instantiation (MAXF 9/17: C5, depth 8, whose 100 000-sphere
 // tree is 12 levels deep) keeps descending until 12 lanes lack a leaf: C5
 // +2.2 % (2: C3 best, 8 there -1.2 %; a run-time threshold cost C3 1 %,
 // profiles/r02/ab_leafwait_r2final.txt)
-constexpr unsigned leaf_wait_for(int maxf) { return maxf > 5 ? 12u : kLeafWait; }
+#ifndef RT_LEAF_WAIT_DEEP
+#define RT_LEAF_WAIT_DEEP 12
+#endif
+constexpr unsigned leaf_wait_for(int maxf) { return maxf > 5 ? (unsigned)RT_LEAF_WAIT_DEEP : kLeafWait; }
 constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
 
-__device__ __forceinline__ float safe_rcp(float x) {
-    return x == 0.0f ? __builtin_copysignf(1e30f, x) : 1.0f / x;
-}
+// 1/x for the slab planes: v_rcp_f32 (1 ulp; 1/+-0 = +-inf, capped by the
+// caller).  The planes need no correctly rounded reciprocal: a relative error
+// of 2^-23 in 1/d moves a plane distance by far less than the 2^-16 D
+// padding of every primitive's box (one v_rcp instead of a ~10-instruction
+// IEEE division per axis and trace)
+__device__ __forceinline__ float safe_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // One leaf's primitives against q: faces (5 words each) then spheres (2 words),
 // rt_bvh.h leaf_records.  Closest: running (best, win); shadow: every valid
@@ -277,7 +297,8 @@ template <bool PRE = false>
 __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, Counters &cnt, float &best, int &win,
                                            bool &opaque, bool faces_only) {
     int v = -link - 1;
-    const float4 *R = p.leafrec + (v >> 8);
+    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(p.leafrec);
+    int off = (v >> 8) * 16;                 // byte offset of the leaf's first record (< 2^27)
     int nfc = (v >> 4) & 15, count = v & 15;
     if (faces_only) count = nfc;             // the leaf's faces come first
     for (int k = 0; k < count; k++) {
@@ -293,10 +314,9 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
         // (w2..w4 are not zeroed when no lane is at a face: only the face
         // branch reads them, and no lane takes it then -- 12 v_mov per leaf
         // primitive saved)
-        const f4v *RV = reinterpret_cast<const f4v *>(R);
-        f4v w0 = RV[0], w1 = RV[1], w2, w3, w4;
+        f4v w0 = bldv(rs, off, 0), w1 = bldv(rs, off, 16), w2, w3, w4;
         if (__ballot(k < nfc))
-            w2 = RV[2], w3 = RV[3], w4 = RV[4];
+            w2 = bldv(rs, off, 32), w3 = bldv(rs, off, 48), w4 = bldv(rs, off, 64);
         else                                 // whatever the registers hold: no instruction
             asm("" : "=v"(w2), "=v"(w3), "=v"(w4));
         asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(w4));
@@ -304,7 +324,7 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
         float4 f2 = make_float4(w2.x, w2.y, w2.z, w2.w), f3 = make_float4(w3.x, w3.y, w3.z, w3.w);
         float4 f4 = make_float4(w4.x, w4.y, w4.z, w4.w);
         if (k < nfc) {
-            R += 5;
+            off += 80;
             key = __float_as_int(f4.y);
             fac = f4.z;
             float a, bb, g;
@@ -312,7 +332,7 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
             h0 = face_test(f0, f1, f2, f3, f4, q.o, q.d, t0, a, bb, g) && (f1.w != 0.0f);
             h1 = false;
         } else {
-            R += 2;
+            off += 32;
             key = __float_as_int(f1.x);
             fac = f1.y;
             RT_COUNT(cnt.stests++);
@@ -441,7 +461,7 @@ __device__ __forceinline__ unsigned child_entry(const ChildPlanes &cp, int i, fl
 template <bool point, unsigned LEAF_WAIT = kLeafWait>
 __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bool org_pass = false, int root = 0,
                           V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
-    // |1/d| capped at 2^100 (1/0 -> 1e30 as before): the quantised planes'
+    // |1/d| capped at 2^100 (1/0 -> 2^100): the quantised planes'
     // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
     // and the cap is conservative: an axis with |d| < 2^-100 moves the ray by
     // less than 2^-100 D along it, far inside the 2^-16 D primitive padding
@@ -593,6 +613,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     // tested before the search from the root: a closest hit found there bounds
     // the search (thi), an opaque occluder ends a shadow ray.  The search
     // visits the leaf again; that changes no result (PRE, leaf_visit).
+    const __amdgpu_buffer_rsrc_t bvh_rs = buffer_rsrc(p.bvh);
     bool ended = false;
     if (!point && org_pass && !faces_only && !q.skipchk && q.self >= 0 && (q.closest || p.shadow_early_out)) {
         leaf_visit<true>(q, p, p.objleaf[q.self], cnt, best, win, opaque, false);
@@ -607,8 +628,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
 #if RT_PROF >= 2
             const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
-            const float4 *N = p.bvh + kNodeF4 * node;
-            float4 w0 = N[0], w1 = N[1], w2 = N[2], w3 = N[3], w4 = N[4];
+            // node = the node's byte offset (rt_scene.cpp): five buffer loads
+            // at immediate offsets from it, no address arithmetic
+            const float4 w0 = bld4(bvh_rs, node, 0), w1 = bld4(bvh_rs, node, 16), w2 = bld4(bvh_rs, node, 32);
+            const float4 w3 = bld4(bvh_rs, node, 48), w4 = bld4(bvh_rs, node, 64);
 #if RT_PROF >= 2
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w3.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;

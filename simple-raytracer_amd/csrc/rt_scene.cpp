@@ -447,6 +447,17 @@ int build_bvh(rt_scene *s, double D) {
         }
         rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     }
+    // device links: an inner node's link is its byte offset in the node array
+    // (the kernel fetches a node with buffer loads at that offset: no address
+    // arithmetic per visit), leaf links stay as they are
+    if (ok && QQ.size() * sizeof(rtbvh::Node4H) > (size_t)INT32_MAX) ok = false;
+    if (ok) {
+        for (auto &z : QQ)
+            for (auto &l : z.link)
+                if (l >= 0) l *= (int32_t)sizeof(rtbvh::Node4H);
+        for (auto &d : dirk)
+            if (d.root >= 0) d.root *= (int)sizeof(rtbvh::Node4H);
+    }
     // The old tree stays valid until the new one is on the device: upload into
     // new buffers first, then swap (a failed rebuild leaves no dangling
     // pointers and no tree marked valid that is not there).
