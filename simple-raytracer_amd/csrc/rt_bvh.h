@@ -305,7 +305,7 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
     Q.nodes[0].max_stack = Q.max_stack;
 }
 
-// Device form of a 4-wide node (80 B, 5 x 16 B; after Ylitie et al. 2017,
+// Device form of a 4-wide node (104 B; after Ylitie et al. 2017,
 // with half-precision instead of 8-bit plane offsets): the node's box origin,
 // one power-of-two scale 2^e for the three axes (stored as the float 2^e: the
 // device forms 2^e / d with one multiply per axis), each child's bounds as
@@ -317,14 +317,23 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
 // padding (rt_kernels.hip).  The device converts h inside the plane FMA
 // (v_fma_mix_f32): no separate conversion instruction per plane, and 2^-11
 // relative resolution (8-bit offsets: 1/255) -- tighter boxes.
+//
+// Per axis the bounds are stored as lo(0,1) lo(2,3) hi(0,1) hi(2,3) lo(0,1)
+// lo(2,3): the 16 bytes at word 0 are (lower, upper) and the 16 bytes at word
+// 2 are (upper, lower) -- a ray reads the window that puts its near planes
+// first (word 2 when its direction along the axis is negative), so the device
+// selects near / far planes by a load offset, not by 4 v_cndmask per axis.
 struct Node4H {
     float origin[3];
     float scale;             // 2^e (-126 <= e <= kQExpMax), one for the three axes
-    uint32_t lo[3][2];       // per axis: lower bounds of children (0, 1), (2, 3)
-    uint32_t hi[3][2];       // per axis: upper bounds
+    uint32_t ax[3][6];       // per axis: lo(0,1) lo(2,3) hi(0,1) hi(2,3) lo(0,1) lo(2,3)
     int32_t link[4];
+    uint32_t lo(int a, int j) const { return ax[a][j]; }
+    uint32_t hi(int a, int j) const { return ax[a][2 + j]; }
 };
-static_assert(sizeof(Node4H) == 80, "node4 device layout");
+static_assert(sizeof(Node4H) == 104, "node4 device layout");
+constexpr int kNodeAxisOff = 16;         // byte offset of axis 0's words; axis a at 16 + 24 a
+constexpr int kNodeLinkOff = 88;         // byte offset of the links
 
 // h in [0, kHMax]: 2048 keeps the offsets where binary16 is integer-exact
 constexpr double kHMax = 2048.0;
@@ -392,7 +401,7 @@ inline bool quantize(const Result4 &Q, std::vector<Node4H> &out) {
         z.scale = (float)sc;                             // exact: a normal power of two
         for (int a = 0; a < 3; a++) {
             auto empty = [&](int i) { return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]); };
-            z.lo[a][0] = z.lo[a][1] = z.hi[a][0] = z.hi[a][1] = 0;
+            for (int w = 0; w < 6; w++) z.ax[a][w] = 0;
             for (int i = 0; i < 4; i++) {
                 uint32_t l = kHalfHMax, h = 0;           // empty slot: inverted box
                 if (!empty(i)) {
@@ -400,9 +409,11 @@ inline bool quantize(const Result4 &Q, std::vector<Node4H> &out) {
                     l = half_round(std::min(kHMax, ((double)n.lo[a][i] - lo[a]) / sc), false);
                     h = half_round(std::min(kHMax, ((double)n.hi[a][i] - lo[a]) / sc), true);
                 }
-                z.lo[a][i / 2] |= l << (16 * (i % 2));
-                z.hi[a][i / 2] |= h << (16 * (i % 2));
+                z.ax[a][i / 2] |= l << (16 * (i % 2));
+                z.ax[a][2 + i / 2] |= h << (16 * (i % 2));
             }
+            z.ax[a][4] = z.ax[a][0];
+            z.ax[a][5] = z.ax[a][1];
         }
     }
     return true;

@@ -257,8 +257,13 @@ __device__ __forceinline__ f4v bldv(__amdgpu_buffer_rsrc_t r, int off, int imm) 
 }
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int off, int imm) { return f4(bldv(r, off, imm)); }
 
-constexpr int kNodeF4 = 5;                       // float4 per 4-wide node (rt_bvh.h Node4H)
-static_assert(kNodeF4 * 16 == sizeof(rtbvh::Node4H), "node layout");
+static_assert(sizeof(rtbvh::Node4H) == 104 && rtbvh::kNodeAxisOff == 16 && rtbvh::kNodeLinkOff == 88, "node layout");
+// uniform float4 at a byte offset (4-byte aligned), via the scalar unit
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ float4 sld4b(const void *p, int off) {
+    f4u v = *(const RT_CONST f4u *)((const RT_CONST char *)p + off);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plane offsets
 // while-while traversal: stop descending when at most this many lanes still
 // look for a leaf (A/B, C3 Mrays/s: 0 -> 5912, 1 -> 5960, 2 -> 5957, 3 -> 5954,
@@ -384,31 +389,29 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
 // the children's offsets from o.  Near / far plane per axis by the ray's
 // octant: t(h) is monotonic in h with the sign of A (= the sign of 1/d), so
 // min(t(lo), t(hi)) is t(near) exactly -- 4 min/max per child, not 10.
+//
+// wa[a]: axis a's window as the ray reads it -- (near 0,1  near 2,3  far 0,1
+// far 2,3) as binary16 pairs: the node stores each axis as lo lo hi hi lo lo,
+// and a ray with a negative direction along the axis loads the 16 bytes from
+// word 2 on (near_window; the root, read through scalar loads, swaps instead).
 struct ChildPlanes {
     float tn[3][4], tf[3][4];                   // [axis][child]: near / far plane
 };
-__device__ __forceinline__ ChildPlanes child_planes(float4 w0, float4 w1, float4 w2, float4 w3, float ix, float iy,
-                                                    float iz, float ox, float oy, float oz, bool neg_x, bool neg_y,
-                                                    bool neg_z) {
+__device__ __forceinline__ ChildPlanes child_planes(float4 w0, const float4 wa[3], float ix, float iy, float iz,
+                                                    float ox, float oy, float oz) {
     // 2^e * (1/d): an exact power-of-two scaling (w0.w = 2^e), finite by the
     // caps (|1/d| <= 2^100, e <= kQExpMax)
     const float A[3] = {ix * w0.w, iy * w0.w, iz * w0.w};
     const float B[3] = {fmaf(w0.x, ix, -ox), fmaf(w0.y, iy, -oy), fmaf(w0.z, iz, -oz)};
-    // lower / upper bounds per axis, two children per word
-    const unsigned lo[3][2] = {{__float_as_uint(w1.x), __float_as_uint(w1.y)},
-                               {__float_as_uint(w1.z), __float_as_uint(w1.w)},
-                               {__float_as_uint(w2.x), __float_as_uint(w2.y)}};
-    const unsigned hi[3][2] = {{__float_as_uint(w2.z), __float_as_uint(w2.w)},
-                               {__float_as_uint(w3.x), __float_as_uint(w3.y)},
-                               {__float_as_uint(w3.z), __float_as_uint(w3.w)}};
-    const bool neg[3] = {neg_x, neg_y, neg_z};
     ChildPlanes cp;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
+        const unsigned nw[2] = {__float_as_uint(wa[a].x), __float_as_uint(wa[a].y)};
+        const unsigned fw[2] = {__float_as_uint(wa[a].z), __float_as_uint(wa[a].w)};
 #pragma unroll
         for (int j = 0; j < 2; j++) {
-            const h2v n = __builtin_bit_cast(h2v, neg[a] ? hi[a][j] : lo[a][j]);
-            const h2v f = __builtin_bit_cast(h2v, neg[a] ? lo[a][j] : hi[a][j]);
+            const h2v n = __builtin_bit_cast(h2v, nw[j]);
+            const h2v f = __builtin_bit_cast(h2v, fw[j]);
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 cp.tn[a][2 * j + e] = fmaf((float)n[e], A[a], B[a]);
@@ -417,6 +420,10 @@ __device__ __forceinline__ ChildPlanes child_planes(float4 w0, float4 w1, float4
         }
     }
     return cp;
+}
+// (lo, hi) window -> the ray's (near, far) window
+__device__ __forceinline__ float4 near_first(float4 w, bool neg) {
+    return neg ? make_float4(w.z, w.w, w.x, w.y) : w;
 }
 
 // Sort key of a child: the bits of its entry distance, kMissKey for a miss or
@@ -469,6 +476,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     const float iy = point ? 1.0f : clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
     const float iz = point ? 1.0f : clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
     const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
+    // per axis: the byte offset of the window with the near planes first
+    // (rt_bvh.h Node4H: lo lo hi hi lo lo -- word 2 on for a negative direction)
+    const int wo_x = neg_x ? 8 : 0, wo_y = neg_y ? 8 : 0, wo_z = neg_z ? 8 : 0;
     const float ox = point ? po.x : q.o.x * ix, oy = point ? po.y : q.o.y * iy, oz = point ? po.z : q.o.z * iz;
     const float tlo = point ? 0.0f : q.tmin - fabsf(q.tmin) * 0x1p-16f;
     // directional shadow ray in a scene with spheres: this pass tests the
@@ -530,7 +540,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     // One 4-wide node (rt_bvh.h Node4H, child_planes): slab-test the
     // children, push the far hits, continue with the nearest, park the first
     // leaf reached.
-    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w3, float4 w4) {
+    auto visit_q = [&](float4 w0, float4 wx, float4 wy, float4 wz, float4 w4) {
 #if RT_PROF
         cnt.trips++;
 #endif
@@ -541,7 +551,8 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         const int top0 = stk[(sp - 1) * kBlock];
         float thi = thi_now();
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
-        const ChildPlanes cp = child_planes(w0, w1, w2, w3, ix, iy, iz, ox, oy, oz, neg_x, neg_y, neg_z);
+        const float4 wa[3] = {wx, wy, wz};
+        const ChildPlanes cp = child_planes(w0, wa, ix, iy, iz, ox, oy, oz);
         unsigned k[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -622,21 +633,26 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     if (point)
         node = root;
     else if (!ended)
-        visit_q(sld4(p.bvh, 0), sld4(p.bvh, 1), sld4(p.bvh, 2), sld4(p.bvh, 3), sld4(p.bvh, 4));
+        visit_q(sld4b(p.bvh, 0), near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff), neg_x),
+                near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff + 24), neg_y),
+                near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff + 48), neg_z), sld4b(p.bvh, rtbvh::kNodeLinkOff));
     for (;;) {
         while (node >= 0) {
 #if RT_PROF >= 2
             const unsigned long long t_a = __builtin_amdgcn_s_memtime();
 #endif
             // node = the node's byte offset (rt_scene.cpp): five buffer loads
-            // at immediate offsets from it, no address arithmetic
-            const float4 w0 = bld4(bvh_rs, node, 0), w1 = bld4(bvh_rs, node, 16), w2 = bld4(bvh_rs, node, 32);
-            const float4 w3 = bld4(bvh_rs, node, 48), w4 = bld4(bvh_rs, node, 64);
+            // at immediate offsets from it; each axis window at the ray's
+            // near-first offset (wo_*: 0 or 8 bytes, per lane)
+            const float4 w0 = bld4(bvh_rs, node, 0), w4 = bld4(bvh_rs, node, rtbvh::kNodeLinkOff);
+            const float4 wx = bld4(bvh_rs, node + wo_x, rtbvh::kNodeAxisOff);
+            const float4 wy = bld4(bvh_rs, node + wo_y, rtbvh::kNodeAxisOff + 24);
+            const float4 wz = bld4(bvh_rs, node + wo_z, rtbvh::kNodeAxisOff + 48);
 #if RT_PROF >= 2
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w3.x) : "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(wz.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
-            visit_q(w0, w1, w2, w3, w4);
+            visit_q(w0, wx, wy, wz, w4);
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
@@ -651,6 +667,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
 #if RT_PROF
             cnt.trips++;
 #endif
+            // the stack top, read while the leaf's primitives are tested (the
+            // leaf visit does not touch the stack)
+            const int top = stk[(sp - 1) * kBlock];
             leaf_visit(q, p, leaf, cnt, best, win, opaque, faces_only);
             leaf = rtbvh::kEmpty;
             if (opaque) {
@@ -660,7 +679,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
             }
             if (node < 0 && node != rtbvh::kEmpty) {
                 leaf = node;
-                node = pop();
+                node = pop_value(top);
             }
         }
         if (node == rtbvh::kEmpty && leaf == rtbvh::kEmpty) break;

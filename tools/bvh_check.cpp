@@ -134,10 +134,14 @@ static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int
         if (!quantize(Q4, QQ)) { printf("FAIL quantize4\n"); return 1; }
         for (size_t k = 0; k < Q.nodes.size(); k++)
             for (int a = 0; a < 3; a++) {
+                if (QQ[k].ax[a][4] != QQ[k].ax[a][0] || QQ[k].ax[a][5] != QQ[k].ax[a][1]) {
+                    printf("FAIL quantize4 window copy\n");     // (hi, lo) window = words 2..5
+                    return 1;
+                }
                 double sc = (double)QQ[k].scale, o = QQ[k].origin[a];
                 for (int i = 0; i < 4; i++) {
-                    double l = half_value((QQ[k].lo[a][i / 2] >> (16 * (i % 2))) & 0xffff);
-                    double h = half_value((QQ[k].hi[a][i / 2] >> (16 * (i % 2))) & 0xffff);
+                    double l = half_value((QQ[k].lo(a, i / 2) >> (16 * (i % 2))) & 0xffff);
+                    double h = half_value((QQ[k].hi(a, i / 2) >> (16 * (i % 2))) & 0xffff);
                     if (Q4.nodes[k].link[i] == kEmpty || !(Q4.nodes[k].lo[a][i] <= Q4.nodes[k].hi[a][i])) {
                         if (!(l > h)) { printf("FAIL quantize4 empty slot\n"); return 1; }
                         continue;
