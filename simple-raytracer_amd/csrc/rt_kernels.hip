@@ -812,39 +812,62 @@ __device__ __forceinline__ void lds_store_phase(const HotR &h) {
     l[LW_META * kBlock] = __uint_as_float(h.meta);
 }
 
+// Cold frame of a node that opened a child (one per recursion level, per
+// lane, in device memory): what the node needs when the child returns.
+//  * head (bytes 0..19): acc, f -- F_t for a refraction child, F_r for a
+//    reflection child -- and the node's meta; then the CHILD's medium stack
+//    (written by the transition in the same line);
+//  * ext (from byte kColdExt on), refraction children only: N, I, obj, eta_i,
+//    eta_t and the hit point -- after a refraction child the node goes on to
+//    its reflection; after a reflection child it is complete and needs only
+//    acc and F_r.
+// A reflection child (~80 % of the child opens) thus dirties only the first
+// 64 bytes of the frame's line for MAXF <= 9, and its return reads only those.
+constexpr int cold_ext(int maxf) { return 20 + 4 * maxf <= 64 ? 64 : (20 + 4 * maxf + 15) / 16 * 16; }
+constexpr int cold_size(int maxf) { return (cold_ext(maxf) + 48 + 63) / 64 * 64; }
 template <int MAXF>
 struct Cold {
-    float4 saved[4];                 // the node's LDS state while a child runs
-    float P[3];                      // its hit point (incidence_object_intersection.point)
-    int stack[MAXF];                 // the CHILD's medium stack (incident_object_stack), object indices:
-                                     // written with the node's own state when it opens the child, so
-                                     // one frame line is dirtied per child open, not two
-    int pad_[(MAXF + 3 + 15) / 16 * 16 - (MAXF + 3)];
+    float4 head;                     // acc.rgb, f
+    unsigned meta;                   // phase:3 | state:1 | stack size:5 | light:23
+    int stack[MAXF];                 // the CHILD's medium stack (incident_object_stack), object indices
+    int pad0_[(cold_ext(MAXF) - 20 - 4 * MAXF) / 4];
+    float4 ext[3];                   // (N, I.x), (I.y, I.z, obj, eta_i), (eta_t, P)
+    int pad1_[(cold_size(MAXF) - cold_ext(MAXF) - 48) / 4];
 };
 static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17>) == 192, "cold frame sizes");
+static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's frame is one 64-B half line");
 
 template <int MAXF>
-__device__ __forceinline__ void cold_save(Cold<MAXF> &c, V3 P, const HotR &h) {
-    f4v *v = reinterpret_cast<f4v *>(c.saved);
-    v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
-    v[1] = f4v{h.I.y, h.I.z, h.dif.r, h.dif.g};
-    v[2] = f4v{h.dif.b, h.acc.r, h.acc.g, h.acc.b};
-    v[3] = f4v{__int_as_float(h.obj), __uint_as_float(h.meta), h.ei, h.et};
-    c.P[0] = P.x, c.P[1] = P.y, c.P[2] = P.z;
+__device__ __forceinline__ void cold_save_head(Cold<MAXF> &c, const HotR &h, float f) {
+    reinterpret_cast<f4v &>(c.head) = f4v{h.acc.r, h.acc.g, h.acc.b, f};
+    c.meta = h.meta;
 }
 template <int MAXF>
-__device__ __forceinline__ V3 cold_restore(const Cold<MAXF> &c, HotR &h) {
-    const f4v *v = reinterpret_cast<const f4v *>(c.saved);
-    f4v a = v[0], b = v[1], d = v[2], e = v[3];
+__device__ __forceinline__ void cold_save_ext(Cold<MAXF> &c, V3 P, const HotR &h) {
+    f4v *v = reinterpret_cast<f4v *>(c.ext);
+    v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
+    v[1] = f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei};
+    v[2] = f4v{h.et, P.x, P.y, P.z};
+}
+// the head: h.acc, h.meta; returns f
+template <int MAXF>
+__device__ __forceinline__ float cold_restore_head(const Cold<MAXF> &c, HotR &h) {
+    const f4v a = reinterpret_cast<const f4v &>(c.head);
+    h.acc = {a.x, a.y, a.z};
+    h.meta = c.meta;
+    return a.w;
+}
+// the rest of a refraction child's parent; returns its hit point
+template <int MAXF>
+__device__ __forceinline__ V3 cold_restore_ext(const Cold<MAXF> &c, HotR &h) {
+    const f4v *v = reinterpret_cast<const f4v *>(c.ext);
+    const f4v a = v[0], b = v[1], d = v[2];
     h.N = {a.x, a.y, a.z};
     h.I = {a.w, b.x, b.y};
-    h.dif = {b.z, b.w, d.x};
-    h.acc = {d.y, d.z, d.w};
-    h.obj = __float_as_int(e.x);
-    h.meta = __float_as_uint(e.y);
-    h.ei = e.z;
-    h.et = e.w;
-    return V3{c.P[0], c.P[1], c.P[2]};
+    h.obj = __float_as_int(b.z);
+    h.ei = b.w;
+    h.et = d.x;
+    return V3{d.y, d.z, d.w};
 }
 
 // Hit record of the winning intersection, recomputed exactly as TraceRay did:
@@ -1235,13 +1258,17 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 set_phase(h, PH_REFL_CHILD);
                 open = true;
             } else {
-                // miss: refl = bkg * F_r; finish this node below
-                h.acc = cadd(h.acc, cmulf(bkg, refl_fresnel(row(p.objs, h.obj), cos_i(h))));
+                // miss: refl = bkg * F_r (F_r in dif.r since the query was
+                // issued); finish this node below
+                h.acc = cadd(h.acc, cmulf(bkg, h.dif.r));
                 set_phase(h, PH_DONE);
             }
         }
         if (open) {                                  // the recursion: save the parent
-            cold_save(ls.cold()[top], q.o, h);
+            Cold<MAXF> &c = ls.cold()[top];
+            // dif.r: F_t (refraction child) or F_r (reflection child)
+            if (h_phase(h) == PH_REFR_CHILD) cold_save_ext(c, q.o, h);
+            cold_save_head(c, h, h.dif.r);
             top++;
         }
     }
@@ -1298,6 +1325,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             if (p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
                 V3 R = vsub(vmul(h.N, (float)(2.0 * (double)cosI)), h.I);
                 closest_query(q, p, R, h.obj);
+                h.dif.r = Fr;                        // for the child's return or the miss (F_t is done with)
                 lds_store_phase(h);
                 ls.top = top;
                 return RK_REFL;
@@ -1312,17 +1340,20 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             return RK_NONE;
         }
         top--;
-        q.o = cold_restore(ls.cold()[top], h);
-        const ObjK &pob = row(p.objs, h.obj);
+        const Cold<MAXF> &pc = ls.cold()[top];
+        const float f = cold_restore_head(pc, h);
         if (h_phase(h) == PH_REFR_CHILD) {           // main.cpp:1072-1083
-            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)h.dif.r)), (float)(1.0 - (double)pob.opacity));
+            q.o = cold_restore_ext(pc, h);
+            h.dif.r = f;                             // F_t
+            const ObjK &pob = row(p.objs, h.obj);
+            C3 tr = cmulf(cmulf(c, (float)(1.0 - (double)f)), (float)(1.0 - (double)pob.opacity));
             h.acc = cadd(h.acc, tr);
             set_phase(h, PH_REFL);
+            lds_store(h);                            // the parent is the top node again
         } else {                                     // PH_REFL_CHILD, main.cpp:1184-1194
-            h.acc = cadd(h.acc, cmulf(c, refl_fresnel(pob, cos_i(h))));
-            set_phase(h, PH_DONE);
+            h.acc = cadd(h.acc, cmulf(c, f));        // f = F_r
+            set_phase(h, PH_DONE);                   // complete: nothing else of it is needed
         }
-        lds_store(h);                                // the parent is the top node again
     }
 }
 
