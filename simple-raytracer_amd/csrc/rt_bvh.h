@@ -323,15 +323,21 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
 // 2 are (upper, lower) -- a ray reads the window that puts its near planes
 // first (word 2 when its direction along the axis is negative), so the device
 // selects near / far planes by a load offset, not by 4 v_cndmask per axis.
+#ifndef RT_NODE_PAD
+#define RT_NODE_PAD 0        // words of padding per node (6: 128-B nodes, one per L2 line)
+#endif
 struct Node4H {
     float origin[3];
     float scale;             // 2^e (-126 <= e <= kQExpMax), one for the three axes
     uint32_t ax[3][6];       // per axis: lo(0,1) lo(2,3) hi(0,1) hi(2,3) lo(0,1) lo(2,3)
     int32_t link[4];
+#if RT_NODE_PAD
+    uint32_t pad_[RT_NODE_PAD];
+#endif
     uint32_t lo(int a, int j) const { return ax[a][j]; }
     uint32_t hi(int a, int j) const { return ax[a][2 + j]; }
 };
-static_assert(sizeof(Node4H) == 104, "node4 device layout");
+static_assert(sizeof(Node4H) == 104 + 4 * RT_NODE_PAD, "node4 device layout");
 constexpr int kNodeAxisOff = 16;         // byte offset of axis 0's words; axis a at 16 + 24 a
 constexpr int kNodeLinkOff = 88;         // byte offset of the links
 
