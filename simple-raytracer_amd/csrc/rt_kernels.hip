@@ -257,7 +257,7 @@ __device__ __forceinline__ f4v bldv(__amdgpu_buffer_rsrc_t r, int off, int imm) 
 }
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int off, int imm) { return f4(bldv(r, off, imm)); }
 
-static_assert(sizeof(rtbvh::Node4H) == 104 && rtbvh::kNodeAxisOff == 16 && rtbvh::kNodeLinkOff == 88, "node layout");
+static_assert(sizeof(rtbvh::Node4H) == 104 + 4 * RT_NODE_PAD && rtbvh::kNodeAxisOff == 16 && rtbvh::kNodeLinkOff == 88, "node layout");
 // uniform float4 at a byte offset (4-byte aligned), via the scalar unit
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ float4 sld4b(const void *p, int off) {
