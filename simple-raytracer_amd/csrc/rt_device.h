@@ -31,8 +31,14 @@ __host__ __device__ __forceinline__ V3 vnorm(V3 a) { return vdiv(a, sqrtf(vdot(a
 __host__ __device__ __forceinline__ V3 vcross(V3 a, V3 b) {
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-// std::clamp(v, 0, 1): NaN passes through (not fminf/fmaxf)
-__device__ __forceinline__ float clamp01(float v) { return (v < 0.0f) ? 0.0f : ((1.0f < v) ? 1.0f : v); }
+// std::clamp(v, 0, 1): NaN passes through (not fminf/fmaxf).  Through the
+// NaN-propagating IEEE maximum / minimum (gfx950 v_maximum3_f32 /
+// v_minimum3_f32): two instructions instead of two compares and two selects;
+// the one difference from std::clamp is -0 -> +0, a sign of zero no later
+// colour operation distinguishes (relaxation 6)
+__device__ __forceinline__ float clamp01(float v) {
+    return __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, 0.0f), 1.0f);
+}
 __device__ __forceinline__ float clampr(float v, float lo, float hi) { return (v < lo) ? lo : ((hi < v) ? hi : v); }
 __device__ __forceinline__ C3 cmulc(C3 a, C3 b) { return {clamp01(b.r * a.r), clamp01(b.g * a.g), clamp01(b.b * a.b)}; }
 __device__ __forceinline__ C3 cmulf(C3 a, float f) { return {clamp01(f * a.r), clamp01(f * a.g), clamp01(f * a.b)}; }

@@ -763,13 +763,17 @@ struct LightW {
 };
 __device__ __forceinline__ LightW light_words(const Params &p, int i) {
     static_assert(sizeof(LightK) == 4 * sizeof(f4v), "LightK = 4 float4");
+    // (the device-memory copy through buffer loads: with two plain loads the
+    // compiler merged the branches into one flat load of a selected address,
+    // which waits on every outstanding vector-memory access as well)
     LightW r;
     if (p.lights_in_lds) {
         const f4v *l = reinterpret_cast<const f4v *>(rt_lds + p.lights_lds) + 4 * i;
         r.w0 = l[0], r.w1 = l[1], r.w2 = l[2], r.w3 = l[3];
     } else {
-        const f4v *g = reinterpret_cast<const f4v *>(p.lights) + 4 * i;
-        r.w0 = g[0], r.w1 = g[1], r.w2 = g[2], r.w3 = g[3];
+        const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(p.lights);
+        r.w0 = bldv(rs, 64 * i, 0), r.w1 = bldv(rs, 64 * i, 16), r.w2 = bldv(rs, 64 * i, 32);
+        r.w3 = bldv(rs, 64 * i, 48);
     }
     return r;
 }
