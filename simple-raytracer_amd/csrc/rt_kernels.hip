@@ -1437,7 +1437,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     int held_kind = RK_NONE;
     bool drained = false;      // wave saw the work counter run out
     unsigned chunk_pos = 0, chunk_end = 0;   // the wave's tile: its unused work items [pos, end)
-    int px = 0, py = 0;
+    unsigned pix_idx = 0;      // the lane's work item (its pixel's (x, y) is recomputed for the store)
 #if RT_PROF >= 2
     cnt.t_fetch = cnt.t_trip = 0;
 #endif
@@ -1464,6 +1464,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             if (!pending) {
                 // the pixel's 12 bytes in one store (global_store_dwordx3)
                 typedef float f3v __attribute__((ext_vector_type(3), aligned(4)));
+                // (x, y) from the work item again: two registers fewer live
+                // across the whole pixel; a pixel list's k-th colour goes to out[3k..]
+                int px = (int)pix_idx, py = 0;
+#ifndef RT_AB_NOPIX
+                if (!p.pix)
+#endif
+                    pixel_xy(p, pix_idx, px, py);
                 *reinterpret_cast<f3v *>(p.out + ((size_t)py * p.W + px) * 3) = f3v{color.r, color.g, color.b};
                 busy = false;
             }
@@ -1505,20 +1512,15 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 if (drained) t_drain = __builtin_amdgcn_s_memrealtime();
 #endif
                 if (!busy) {
-                    unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
+                    // idle lanes below this one (v_mbcnt: no per-lane mask kept in registers)
+                    unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
                     unsigned idx = rank < split ? base + rank : nbase + (rank - split);
                     if (idx < p.total) {
+                        int px, py;
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
                         q.d = primary_dir(p, px, py);
-#ifdef RT_AB_NOPIX
-                        if (false) {
-#else
-                        if (p.pix) {             // the list's k-th colour goes to out[3k..]
-#endif
-                            px = (int)idx;
-                            py = 0;
-                        }
+                        pix_idx = idx;
                         q.tmin = 0.0f;               // primary rays accept any t > 0 (main.cpp:736)
                         q.tmax = kFltMax;
                         q.unb = false;
