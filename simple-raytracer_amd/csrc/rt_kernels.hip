@@ -1229,10 +1229,14 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
             C3 lc = {lw1.x, lw1.y, lw1.z};
             h.acc = cadd(h.acc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
             h.meta += 1u << 9;                       // next light
+            // stored at once, in the block that computed it: kept in registers
+            // across the other phases' code of the shading step, the colour
+            // was spilled to scratch and reloaded -- a reload whose vmcnt wait
+            // also waited for the frame stores of lanes that opened a child
+            lds_store_light(h);
             if (light + 1 < p.nl) {
                 // next light's shadow ray from the same point: origin, self
                 // and cumulative mask are already in q (main.cpp:885-928)
-                lds_store_light(h);
                 // (opaque index: reusing this light's address for the next
                 // one kept a 64-bit pointer live -- and spilled -- across the
                 // shading code)
