@@ -1002,7 +1002,6 @@ struct Medium {
 
 __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m) {
     const HitRec hr = hit_geometry(p, obj, o, d, t);
-    const V3 P = hr.P;
     V3 N = hr.N;
     const ObjK &ob = row(p.objs, obj);
     V3 I = vmul(d, -1.0f);
@@ -1046,7 +1045,12 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
     h.ei = m.ei;
     h.et = m.et;
     lds_store(h);
-    return P;
+    // the hit point again, as hit_geometry computed it (the same operations on
+    // the same inputs: the same value): held across the texture and shading
+    // code above it was spilled to scratch
+    float tt = t;
+    asm volatile("" : "+v"(tt));
+    return vadd(o, vmul(d, tt));
 }
 
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
