@@ -140,6 +140,9 @@ enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 #ifndef RT_PROF
 #define RT_PROF 0                        // 1: per-wave cycle/occupancy counters in stats[9..15]
 #endif
+#ifndef RT_PRIO
+#define RT_PRIO 1                        // 1: shading steps at wave priority 2 (render_kernel)
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif
