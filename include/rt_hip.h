@@ -205,10 +205,11 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * "lds_stack" (12..16, default 14: BVH stack entries kept in LDS per lane;
  * deeper stacks spill to device memory -- a test knob), "bvh_leaf" (largest
  * leaf), "bvh_collapse" (0 greedy, 1 SAH-optimal 4-wide collapse), "bvh_node"
- * (the collapse's node cost x1000),
+ * (the collapse's node cost x1000), "bvh_threads" (host threads of the BVH
+ * build: 0 automatic -- the process's CPUs, at most OMP_NUM_THREADS and 16 --,
+ * 1 serial; every count builds the same tree),
  * "chunk" (0..4096: pixels a wave takes from the work counter at a time,
- * 0 = as many as it has idle lanes; default: 64, one 8x8 tile, when some
- * material reflects or refracts, else 0 -- never changes the image),
+ * default 0 = as many as it has idle lanes -- never changes the image),
  * "refill_min" (1..64: idle lanes a wave gathers before it refills them;
  * default 32 when some material reflects or refracts, 48 above depth 4,
  * 64 with primary and shadow rays only), "gate_x"
@@ -237,6 +238,14 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * across it meets, x1000), [42] BVH stack entries in LDS, [43] lights staged
  * in LDS (1) or read from device memory (0).  n <= 48. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
+
+/* Debug: the last render's per-wave timeline, RT_PROF builds only (others
+ * return RT_E_INVALID).  8 words per wave of the launch: [0] wave start,
+ * [1] prologue done, [2] work counter seen drained (0: never), [3] wave end
+ * (100 MHz ticks, the clock of counters [24..29]), [4] HW_ID, [5] XCC_ID,
+ * [6] outer iterations (trace steps), [7] refill batches.  Copies at most n
+ * words; returns the number copied. */
+int rt_scene_debug_wavelog(rt_scene *scene, unsigned long long *out, int n);
 
 const char *rt_strerror(int code);
 

@@ -22,9 +22,12 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <functional>
+#include <thread>
 #include <vector>
 
 namespace rtbvh {
@@ -220,11 +223,16 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
         first[n] = num > 0 ? lo : 0, cnt[n] = num, psum[n] = s;
         float *Cn = &C[(size_t)n * (W + 1)];
         int8_t *Dn = &D[(size_t)n * (W + 1)];
+        // the children's costs as 1..W units, once (cost() of a leaf child
+        // is its area times its primitives' cost, whatever the units)
+        float cc[2][W + 1];
+        for (int side = 0; side < 2; side++)
+            for (int k = 1; k <= W; k++) cc[side][k] = (ch[side].link >= 0 || k == 1) ? cost(ch[side], k) : cc[side][1];
         auto dist = [&](int j, int &kbest) {
             float best = INFINITY;
             kbest = 1;
             for (int k = 1; k < j; k++) {
-                float c = cost(ch[0], k) + cost(ch[1], j - k);
+                float c = cc[0][k] + cc[1][j - k];
                 if (c < best) best = c, kbest = k;
             }
             return best;
@@ -241,9 +249,13 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
             else Cn[i] = Cn[i - 1], Dn[i] = 0;
         }
     }
+    struct Units {                                    // at most W units of one node
+        Ref r[W];
+        int m = 0;
+        void push_back(const Ref &x) { r[m++] = x; }
+    };
     // subtree `r` as at most i units
-    std::function<void(const Ref &, int, std::vector<Ref> &)> gather = [&](const Ref &r, int i,
-                                                                           std::vector<Ref> &out) {
+    std::function<void(const Ref &, int, Units &)> gather = [&](const Ref &r, int i, Units &out) {
         if (r.link < 0) {
             out.push_back(r);
             return;
@@ -275,10 +287,11 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
                 if (c < best) best = c, k = j;
             }
         }
-        std::vector<Ref> ch;
-        gather(ch2[0], k, ch);
-        gather(ch2[1], W - k, ch);
-        const int m = (int)ch.size();
+        Units us;
+        gather(ch2[0], k, us);
+        gather(ch2[1], W - k, us);
+        const Ref *ch = us.r;
+        const int m = us.m;
         int qi = (int)Q.nodes.size();
         Q.nodes.emplace_back();
         Q.depth = std::max(Q.depth, depth);
@@ -359,14 +372,31 @@ inline uint16_t half_bits(double r) {
     return (uint16_t)(((E + 15) << 10) | ((uint32_t)std::ldexp(r, 10 - E) - 1024u));
 }
 // the largest binary16 value <= v (up = false) or the smallest >= v (up =
-// true), for v in [0, kHMax]
+// true), for v in [0, kHMax]: v = m * 2^u with u the binary16 ulp exponent
+// of v's binade (2^-24 below 2^-14), m rounded down / up to an integer; a
+// carry to m = 2^11 moves to the next binade.  Bit operations on the double:
+// exact, and the same bits as the frexp / ldexp formulation (half_bits(m 2^u))
 inline uint16_t half_round(double v, bool up) {
     if (!(v > 0)) return 0;
-    int k;
-    std::frexp(v, &k);
-    const double ulp = std::ldexp(1.0, std::max(k - 1, -14) - 10);
-    const double m = up ? std::ceil(v / ulp) : std::floor(v / ulp);
-    return half_bits(m * ulp);               // exact: m < 2^12, ulp a power of two
+    uint64_t b;
+    std::memcpy(&b, &v, sizeof b);
+    const int E = (int)((b >> 52) & 0x7ff) - 1023;          // v normal: v in [2^E, 2^(E+1)), E <= 11
+    const int u = std::max(E, -14) - 10;                     // ulp exponent
+    // m = v / 2^u as a 53-bit fixed-point integer part: shift the significand
+    const uint64_t sig = (b & ((uint64_t(1) << 52) - 1)) | (uint64_t(1) << 52);   // v = sig * 2^(E - 52)
+    const int sh = 52 - (E - u);                             // v / 2^u = sig >> sh (sh >= 42 for u >= E - 10)
+    uint64_t m;
+    if (sh >= 64) {
+        m = up ? 1 : 0;                                      // v < 2^u (v > 0): rounds to 0 or one ulp
+    } else {
+        m = sig >> sh;
+        if (up && (sig & ((uint64_t(1) << sh) - 1))) m++;
+    }
+    int ue = u;
+    if (m == 2048) m = 1024, ue++;                           // carry into the next binade
+    if (m == 0) return 0;
+    if (m < 1024) return (uint16_t)m;                        // subnormal (ue = -24)
+    return (uint16_t)(((ue + 10 + 15) << 10) | (uint32_t)(m - 1024));
 }
 // value of binary16 bits (non-negative)
 inline double half_value(uint16_t b) {
@@ -374,55 +404,86 @@ inline double half_value(uint16_t b) {
     return E == 0 ? std::ldexp((double)m, -24) : std::ldexp(1024.0 + m, E - 25);
 }
 
-// Returns false if a child box is not finite (NaN/inf geometry) or a node is
-// too large for kQExpMax: the caller then uses the brute-force scan.
-inline bool quantize(const Result4 &Q, std::vector<Node4H> &out) {
-    out.assign(Q.nodes.size(), Node4H{});
-    for (size_t k = 0; k < Q.nodes.size(); k++) {
-        const Node4 &n = Q.nodes[k];
-        Node4H &z = out[k];
-        for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
-        double lo[3], hi[3];
-        int e = -126;
-        for (int a = 0; a < 3; a++) {
-            auto empty = [&](int i) {              // no slot, or an empty leaf (inverted box)
-                return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]);
-            };
-            lo[a] = INFINITY, hi[a] = -INFINITY;
-            for (int i = 0; i < 4; i++) {
-                if (empty(i)) continue;
-                if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
-                lo[a] = std::min(lo[a], (double)n.lo[a][i]);
-                hi[a] = std::max(hi[a], (double)n.hi[a][i]);
-            }
-            if (!(lo[a] <= hi[a])) lo[a] = hi[a] = 0.0;  // no child at all
-            z.origin[a] = (float)lo[a];                  // exact: lo is a float
-            // smallest scale 2^e with kHMax * 2^e >= every axis' extent (normal
-            // floats only); binary16 is floating point, so a shorter axis keeps
-            // 11 significant bits in its offsets
-            while (e < 127 && std::ldexp(kHMax, e) < hi[a] - lo[a]) e++;
+// Run f(begin, end) over [0, n) in `threads` contiguous slices (the
+// results must not depend on the split).
+template <class F>
+inline void parallel_ranges(size_t n, int threads, F f) {
+    const size_t t = (size_t)std::max(1, std::min<int>(threads, (int)((n + 2047) / 2048)));
+    if (t <= 1) {
+        f((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (size_t k = 1; k < t; k++) pool.emplace_back(f, n * k / t, n * (k + 1) / t);
+    f((size_t)0, n / t);
+    for (auto &th : pool) th.join();
+}
+
+// One node of quantize; false if a child box is not finite or the node is too
+// large for kQExpMax.
+inline bool quantize_node(const Node4 &n, Node4H &z) {
+    z = Node4H{};
+    for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
+    double lo[3], hi[3];
+    int e = -126;
+    for (int a = 0; a < 3; a++) {
+        auto empty = [&](int i) {              // no slot, or an empty leaf (inverted box)
+            return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]);
+        };
+        lo[a] = INFINITY, hi[a] = -INFINITY;
+        for (int i = 0; i < 4; i++) {
+            if (empty(i)) continue;
+            if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
+            lo[a] = std::min(lo[a], (double)n.lo[a][i]);
+            hi[a] = std::max(hi[a], (double)n.hi[a][i]);
         }
-        if (e > kQExpMax) return false;
-        const double sc = std::ldexp(1.0, e);
-        z.scale = (float)sc;                             // exact: a normal power of two
-        for (int a = 0; a < 3; a++) {
-            auto empty = [&](int i) { return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]); };
-            for (int w = 0; w < 6; w++) z.ax[a][w] = 0;
-            for (int i = 0; i < 4; i++) {
-                uint32_t l = kHalfHMax, h = 0;           // empty slot: inverted box
-                if (!empty(i)) {
-                    // exact in double: float differences, power-of-two scale
-                    l = half_round(std::min(kHMax, ((double)n.lo[a][i] - lo[a]) / sc), false);
-                    h = half_round(std::min(kHMax, ((double)n.hi[a][i] - lo[a]) / sc), true);
-                }
-                z.ax[a][i / 2] |= l << (16 * (i % 2));
-                z.ax[a][2 + i / 2] |= h << (16 * (i % 2));
-            }
-            z.ax[a][4] = z.ax[a][0];
-            z.ax[a][5] = z.ax[a][1];
+        if (!(lo[a] <= hi[a])) lo[a] = hi[a] = 0.0;  // no child at all
+        z.origin[a] = (float)lo[a];                  // exact: lo is a float
+        // smallest scale 2^e with kHMax * 2^e >= every axis' extent (normal
+        // floats only); binary16 is floating point, so a shorter axis keeps
+        // 11 significant bits in its offsets.  ext / kHMax = m 2^k with m in
+        // [1/2, 1) (exact: a power-of-two division): 2^e >= it from e = k,
+        // or k - 1 when m = 1/2
+        const double ext = hi[a] - lo[a];
+        if (ext > std::ldexp(kHMax, e)) {
+            int k;
+            const double m = std::frexp(ext / kHMax, &k);
+            e = std::min(127, std::max(e, m == 0.5 ? k - 1 : k));
         }
     }
+    if (e > kQExpMax) return false;
+    const double sc = std::ldexp(1.0, e);
+    z.scale = (float)sc;                             // exact: a normal power of two
+    for (int a = 0; a < 3; a++) {
+        auto empty = [&](int i) { return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]); };
+        for (int w = 0; w < 6; w++) z.ax[a][w] = 0;
+        for (int i = 0; i < 4; i++) {
+            uint32_t l = kHalfHMax, h = 0;           // empty slot: inverted box
+            if (!empty(i)) {
+                // exact in double: float differences, power-of-two scale
+                l = half_round(std::min(kHMax, ((double)n.lo[a][i] - lo[a]) / sc), false);
+                h = half_round(std::min(kHMax, ((double)n.hi[a][i] - lo[a]) / sc), true);
+            }
+            z.ax[a][i / 2] |= l << (16 * (i % 2));
+            z.ax[a][2 + i / 2] |= h << (16 * (i % 2));
+        }
+        z.ax[a][4] = z.ax[a][0];
+        z.ax[a][5] = z.ax[a][1];
+    }
     return true;
+}
+
+// Returns false if a child box is not finite (NaN/inf geometry) or a node is
+// too large for kQExpMax: the caller then uses the brute-force scan.  Nodes
+// are independent: `threads` host threads share them.
+inline bool quantize(const Result4 &Q, std::vector<Node4H> &out, int threads = 1) {
+    out.assign(Q.nodes.size(), Node4H{});
+    std::atomic<bool> ok{true};
+    parallel_ranges(Q.nodes.size(), threads, [&](size_t b, size_t e) {
+        for (size_t k = b; k < e; k++)
+            if (!quantize_node(Q.nodes[k], out[k])) ok.store(false);
+    });
+    return ok.load();
 }
 
 // Renumber Q's nodes breadth-first (root stays 0), so that the top levels of
@@ -476,22 +537,36 @@ inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace
             int32_t l = n.link[i];
             if (l >= 0 || l == kEmpty) continue;
             int v = -l - 1, first = v >> 4, count = v & 15;
-            std::vector<int32_t> ks(keys.begin() + first, keys.begin() + first + count);
-            std::stable_sort(ks.begin(), ks.end(), [&](int32_t a, int32_t b) {
-                bool fa = is_face(a), fb = is_face(b);
-                return fa != fb ? fa : a < b;
-            });
+            // faces first, each kind in key order (a stable insertion sort:
+            // count <= 15)
+            int32_t ks[16];
+            bool fs[16];
+            for (int q = 0; q < count; q++) {
+                const int32_t k = keys[(size_t)first + q];
+                const bool f = is_face(k);
+                int w = q;
+                while (w > 0 && (fs[w - 1] != f ? f : k < ks[w - 1])) ks[w] = ks[w - 1], fs[w] = fs[w - 1], w--;
+                ks[w] = k, fs[w] = f;
+            }
             int nfaces = 0;
-            for (int32_t k : ks) nfaces += is_face(k) ? 1 : 0;
+            for (int q = 0; q < count; q++) nfaces += fs[q] ? 1 : 0;
             // off <= 2^23 - 2 keeps every link above INT_MIN + 256 (device sentinels)
             if (words >= (size_t(1) << 23) - 1) return false;
             n.link[i] = -(1 + (int32_t)((words << 8) | (size_t)(nfaces << 4) | (size_t)count));
-            for (int32_t k : ks) words += (size_t)emit(k);
+            for (int q = 0; q < count; q++) words += (size_t)emit(ks[q]);
         }
     }
     return true;
 }
 
+// Binned SAH builder of the binary tree.  Nodes are numbered depth-first
+// (a node, then its left subtree, then its right subtree: children have larger
+// indices than their parent, which collapse_sah relies on).  The builder
+// reorders the primitive array itself (sequential passes over each range,
+// not an index indirection), in the order an index permutation would take.
+// With threads > 1 large subtrees are built on their own threads into their
+// own node arrays and spliced back in that order: the tree is the same for
+// every thread count (tests/test_bvh_host.py checks it bit for bit).
 class Builder {
    public:
 #ifndef RT_SAH_BINS
@@ -500,37 +575,61 @@ class Builder {
     static constexpr int kBins = RT_SAH_BINS;
     int max_leaf = 8;                       // SAH leaves (<= 15 fits the link encoding)
     float trav_cost = 1.0f;                 // SAH cost of one node visit, in sphere tests
+    int threads = 1;                        // host threads (subtree tasks)
     static constexpr int kSahDepth = 22;    // deeper: object-median splits (bounded depth)
     static constexpr int kMaxDepth = 64;    // binary depth cap (object-median splits below kSahDepth keep it low)
+    static constexpr int kForkMin = 2048;   // smallest subtree built on a thread of its own
 
+    // prims: reordered by the build (leaf order)
     explicit Builder(std::vector<Prim> &prims) : P(prims) {}
 
     // Returns false if the tree would be deeper than kMaxDepth.
     bool build(Result &R) {
-        out = &R;
         R = Result();
         if (P.empty()) return true;
-        idx.resize(P.size());
-        for (size_t i = 0; i < P.size(); i++) idx[i] = (int)i;
-        R.nodes.reserve(P.size());
-        R.nodes.emplace_back();                       // the root is node 0
-        int mid = split_point(0, (int)P.size(), 1);
-        if (mid < 0) mid = (int)P.size();             // everything in one leaf
-        int32_t l = mid > 0 ? build_range(0, mid, 2) : leaf_link(0, 0);
-        int32_t r = mid < (int)P.size() ? build_range(mid, (int)P.size(), 2) : leaf_link(0, 0);
-        set_child(R.nodes[0], 0, bounds(0, mid), l);
-        set_child(R.nodes[0], 1, bounds(mid, (int)P.size()), r);
-        R.depth = std::max(R.depth, 1);
+        const int n = (int)P.size();
+        forks.store(std::max(0, threads - 1));
+        Sub S;
+        S.nodes.reserve(P.size());
+        S.nodes.emplace_back();                       // the root is node 0
+        Range all = range(0, n);
+        int mid = split_point(0, n, 1, all);
+        if (mid < 0) mid = n;                         // everything in one leaf
+        const Range lr = range(0, mid), rr = range(mid, n);
+        int32_t l = leaf_link(0, 0), r = leaf_link(0, 0);
+        children(0, mid, n, 2, lr, rr, l, r, S, mid > 0, mid < n);
+        set_child(S.nodes[0], 0, lr.box, l);
+        set_child(S.nodes[0], 1, rr.box, r);
+        R.nodes.swap(S.nodes);
+        R.depth = std::max(S.depth, 1);
         R.keys.resize(P.size());
         R.costs.resize(P.size());
-        for (size_t i = 0; i < P.size(); i++) R.keys[i] = P[idx[i]].key, R.costs[i] = P[idx[i]].cost;
+        for (size_t i = 0; i < P.size(); i++) R.keys[i] = P[i].key, R.costs[i] = P[i].cost;
         return R.depth <= kMaxDepth;
     }
 
    private:
     std::vector<Prim> &P;
-    std::vector<int> idx;
-    Result *out = nullptr;
+    std::atomic<int> forks{0};              // threads still free for subtrees
+
+    struct Sub {                            // a subtree's nodes, numbered from 0
+        std::vector<Node> nodes;
+        int depth = 0;
+    };
+    struct Range {                          // a range's bounds, centroid bounds and cost
+        Box box, cbox;
+        float cost = 0.0f;                  // summed in array order
+    };
+
+    Range range(int a, int b) const {
+        Range r;
+        for (int i = a; i < b; i++) {
+            r.box.grow(P[i].box);
+            r.cbox.grow(P[i].c);
+            r.cost += P[i].cost;
+        }
+        return r;
+    }
 
     static void set_child(Node &n, int side, const Box &b, int32_t link) {
         if (side == 0) {
@@ -543,93 +642,168 @@ class Builder {
         n.link[side] = link;
     }
 
-    Box bounds(int a, int b) const {
-        Box x;
-        for (int i = a; i < b; i++) x.grow(P[idx[i]].box);
-        return x;
+    // The best binned split of one axis, in the order a dense sweep over
+    // every bin visits it (k from kBins - 1 down, strict '<'): updates (best,
+    // best_axis, best_bin).  bins[0..m) are the non-empty bins, ascending
+    // (dense: m = kBins, bins = 0..kBins-1).  Every k in (bins[j-1], bins[j]]
+    // splits the same sets at the same cost and the dense sweep meets
+    // k = bins[j] first; empty bins add +0 to the cost sums (exact), so both
+    // forms choose the same split.
+    static void sweep(const Box *bb, const float *cc, const int *bins, int m, int ax, float &best, int &best_axis,
+                      int &best_bin) {
+        // left areas only (the boxes themselves are not needed after it);
+        // no default-constructed box arrays: this runs once per axis for
+        // every node of a tree built down to single primitives
+        float la[kBins];
+        float lc[kBins];
+        Box acc;
+        float c = 0;
+        for (int j = 0; j < m; j++) {
+            acc.grow(bb[j]);
+            c += cc[j];
+            la[j] = acc.area();
+            lc[j] = c;
+        }
+        acc = Box();
+        c = 0;
+        for (int j = m - 1; j > 0; j--) {
+            acc.grow(bb[j]);
+            c += cc[j];
+            if (lc[j - 1] == 0 || c == 0) continue;
+            float s = la[j - 1] * lc[j - 1] + acc.area() * c;
+            if (s < best) best = s, best_axis = ax, best_bin = bins[j];
+        }
     }
 
-    // Partition [a, b) and return the split position, or -1 for "make a leaf".
-    int split_point(int a, int b, int depth) {
+    // kBins boxes, not constructed (filled before they are read)
+    struct BoxStore {
+        union {
+            Box b[kBins];
+        };
+        BoxStore() {}
+    };
+
+    static int bin_of(const Prim &p, int ax, float lo, float scale) {
+        return std::min(kBins - 1, std::max(0, (int)((p.c[ax] - lo) * scale)));
+    }
+
+    // Partition [a, b) (its Range ri) and return the split position, or -1
+    // for "make a leaf".
+    int split_point(int a, int b, int depth, const Range &ri) {
         int n = b - a;
         if (n <= 1) return -1;
-        Box cb;
-        float cost_leaf = 0;
-        for (int i = a; i < b; i++) {
-            cb.grow(P[idx[i]].c);
-            cost_leaf += P[idx[i]].cost;
-        }
+        const Box &cb = ri.cbox;
+        const float cost_leaf = ri.cost;
         if (depth > kSahDepth) {
             if (n <= 2) return -1;
             int ax = 0;
             for (int k = 1; k < 3; k++)
                 if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
             int mid = a + n / 2;
-            std::nth_element(idx.begin() + a, idx.begin() + mid, idx.begin() + b,
-                             [&](int x, int y) { return P[x].c[ax] < P[y].c[ax]; });
+            std::nth_element(P.begin() + a, P.begin() + mid, P.begin() + b,
+                             [&](const Prim &x, const Prim &y) { return x.c[ax] < y.c[ax]; });
             return mid;
         }
         float best = INFINITY;
         int best_axis = -1, best_bin = -1;
+        float lo[3], scale[3];
+        bool live[3];
         for (int ax = 0; ax < 3; ax++) {
-            float lo = cb.lo[ax], hi = cb.hi[ax];
-            if (!(hi > lo)) continue;
-            float scale = kBins / (hi - lo);
-            Box bb[kBins];
-            float cc[kBins] = {0};
-            for (int i = a; i < b; i++) {
-                const Prim &p = P[idx[i]];
-                int k = std::min(kBins - 1, std::max(0, (int)((p.c[ax] - lo) * scale)));
-                bb[k].grow(p.box);
-                cc[k] += p.cost;
-            }
-            Box left[kBins];
-            float lc[kBins];
-            Box acc;
-            float c = 0;
-            for (int k = 0; k < kBins; k++) {
-                acc.grow(bb[k]);
-                c += cc[k];
-                left[k] = acc;
-                lc[k] = c;
-            }
-            acc = Box();
-            c = 0;
-            for (int k = kBins - 1; k > 0; k--) {
-                acc.grow(bb[k]);
-                c += cc[k];
-                if (lc[k - 1] == 0 || c == 0) continue;
-                float s = left[k - 1].area() * lc[k - 1] + acc.area() * c;
-                if (s < best) best = s, best_axis = ax, best_bin = k;
-            }
+            lo[ax] = cb.lo[ax];
+            live[ax] = cb.hi[ax] > lo[ax];
+            scale[ax] = live[ax] ? kBins / (cb.hi[ax] - lo[ax]) : 0.0f;
         }
-        float area = bounds(a, b).area();
+        if (n < kBins / 2) {
+            // few primitives: only their bins, sorted per axis
+            for (int ax = 0; ax < 3; ax++) {
+                if (!live[ax]) continue;
+                BoxStore bb;
+                float cc[kBins];
+                int bins[kBins];
+                int key[kBins];
+                int m = 0;
+                for (int i = 0; i < n; i++) key[i] = (bin_of(P[a + i], ax, lo[ax], scale[ax]) << 8) | i;
+                std::sort(key, key + n);
+                for (int t = 0; t < n; t++) {
+                    const int k = key[t] >> 8;
+                    const Prim &p = P[a + (key[t] & 255)];
+                    if (m == 0 || bins[m - 1] != k) bins[m] = k, bb.b[m] = Box(), cc[m] = 0.0f, m++;
+                    bb.b[m - 1].grow(p.box);
+                    cc[m - 1] += p.cost;
+                }
+                sweep(bb.b, cc, bins, m, ax, best, best_axis, best_bin);
+            }
+        } else {
+            // one pass over the range bins all three axes
+            Box bb[3][kBins];
+            float cc[3][kBins];
+            int bins[kBins];
+            for (int k = 0; k < kBins; k++) cc[0][k] = cc[1][k] = cc[2][k] = 0.0f, bins[k] = k;
+            for (int i = a; i < b; i++) {
+                const Prim &p = P[i];
+                for (int ax = 0; ax < 3; ax++) {
+                    const int k = bin_of(p, ax, lo[ax], scale[ax]);
+                    bb[ax][k].grow(p.box);
+                    cc[ax][k] += p.cost;
+                }
+            }
+            for (int ax = 0; ax < 3; ax++)
+                if (live[ax]) sweep(bb[ax], cc[ax], bins, kBins, ax, best, best_axis, best_bin);
+        }
+        float area = ri.box.area();
         float split_cost = (best_axis >= 0 && area > 0) ? trav_cost + best / area : INFINITY;
         if (n <= max_leaf && split_cost >= cost_leaf) return -1;
         if (best_axis < 0) {                         // all centroids coincide
             if (n <= 15) return -1;
             return a + n / 2;
         }
-        float lo = cb.lo[best_axis], scale = kBins / (cb.hi[best_axis] - lo);
-        auto it = std::partition(idx.begin() + a, idx.begin() + b, [&](int i) {
-            int k = std::min(kBins - 1, std::max(0, (int)((P[i].c[best_axis] - lo) * scale)));
-            return k < best_bin;
-        });
-        int mid = (int)(it - idx.begin());
+        const float blo = lo[best_axis], bsc = scale[best_axis];
+        auto it = std::partition(P.begin() + a, P.begin() + b,
+                                 [&](const Prim &p) { return bin_of(p, best_axis, blo, bsc) < best_bin; });
+        int mid = (int)(it - P.begin());
         if (mid == a || mid == b) mid = a + n / 2;
         return mid;
     }
 
-    int32_t build_range(int a, int b, int depth) {
-        out->depth = std::max(out->depth, depth);
-        int mid = split_point(a, b, depth);
+    // The two children of a node over [a, mid) and [mid, b): on this thread,
+    // or the left one on a thread of its own when the range is large
+    void children(int a, int mid, int b, int depth, const Range &lr, const Range &rr, int32_t &l, int32_t &r,
+                  Sub &out, bool has_l = true, bool has_r = true) {
+        if (has_l && has_r && b - a >= kForkMin && forks.fetch_sub(1) > 0) {
+            Sub L, Rs;
+            std::thread t([&] { l = build_range(a, mid, depth, lr, L); });
+            r = build_range(mid, b, depth, rr, Rs);
+            t.join();
+            const int offL = (int)out.nodes.size(), offR = offL + (int)L.nodes.size();
+            auto splice = [&](Sub &S, int off) {
+                for (Node nd : S.nodes) {
+                    for (int k = 0; k < 2; k++)
+                        if (nd.link[k] >= 0) nd.link[k] += off;
+                    out.nodes.push_back(nd);
+                }
+                out.depth = std::max(out.depth, S.depth);
+            };
+            splice(L, offL);
+            splice(Rs, offR);
+            if (l >= 0) l += offL;
+            if (r >= 0) r += offR;
+            return;
+        }
+        if (has_l) l = build_range(a, mid, depth, lr, out);
+        if (has_r) r = build_range(mid, b, depth, rr, out);
+    }
+
+    int32_t build_range(int a, int b, int depth, const Range &ri, Sub &out) {
+        out.depth = std::max(out.depth, depth);
+        int mid = split_point(a, b, depth, ri);
         if (mid < 0) return leaf_link(a, b - a);
-        int ni = (int)out->nodes.size();
-        out->nodes.emplace_back();
-        int32_t l = build_range(a, mid, depth + 1);
-        int32_t r = build_range(mid, b, depth + 1);
-        set_child(out->nodes[ni], 0, bounds(a, mid), l);
-        set_child(out->nodes[ni], 1, bounds(mid, b), r);
+        int ni = (int)out.nodes.size();
+        out.nodes.emplace_back();
+        const Range lr = range(a, mid), rr = range(mid, b);
+        int32_t l, r;
+        children(a, mid, b, depth + 1, lr, rr, l, r, out);
+        set_child(out.nodes[ni], 0, lr.box, l);
+        set_child(out.nodes[ni], 1, rr.box, r);
         return ni;
     }
 };

@@ -181,6 +181,17 @@ constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.
 constexpr int kOrgFirst = RT_ORG_FIRST;
 constexpr double kOrgDensity = 32.0;     // objects met by a line across the scene (C3 ~3, C5 ~200)
 constexpr int kNStats = 48;              // counter slots (rt_scene_debug_counters; the device writes 0..39)
+// RT_PROF builds: a per-wave timeline after the counters (rt_scene_debug_wavelog),
+// kWaveLogWords words per wave: launch start, prologue done, work drained (0:
+// never saw it), end (100 MHz ticks), HW_ID, XCC_ID, outer iterations, refills
+#if RT_PROF
+constexpr int kWaveLogWords = 8;
+constexpr int kWaveLogMax = 16384;       // waves (grid x kBlock / 64 <= 1280 x 4 on MI355X)
+#else
+constexpr int kWaveLogWords = 8;
+constexpr int kWaveLogMax = 0;
+#endif
+constexpr int kStatsAlloc = kNStats + kWaveLogWords * kWaveLogMax;
 constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS (rt_kernels.hip LW_*)
 
 // ---------------------------------------------------------------------------

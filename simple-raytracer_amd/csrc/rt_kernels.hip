@@ -1459,6 +1459,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
     unsigned long long pc_mixed = 0;     // trace steps with primary and secondary/shadow searches together
     unsigned long long t_drain = 0;
+    unsigned long long n_refill = 0;
+    const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
 #endif
     for (;;) {
 #if RT_PROF
@@ -1517,6 +1519,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     unsigned g = 0;
                     const unsigned take = max(p.chunk, n - split);
                     if (lane == leader) g = atomicAdd(p.work, take);
+#if RT_PROF
+                    n_refill++;
+#endif
                     nbase = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
                     chunk_pos = nbase + (n - split);
                     chunk_end = nbase + take;
@@ -1688,6 +1693,20 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&st[36], (unsigned long long)cnt.trips_kind[0]);
     atomicAdd(&st[37], (unsigned long long)cnt.trips_kind[1]);
     atomicAdd(&st[38], (unsigned long long)cnt.trips_kind[2]);
+    {
+        const unsigned w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+        if (lane == 0 && w < (unsigned)kWaveLogMax) {
+            unsigned long long *wl = st + kNStats + (size_t)w * kWaveLogWords;
+            wl[0] = t_start;
+            wl[1] = t_loop;
+            wl[2] = t_drain;
+            wl[3] = t_end;
+            wl[4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+            wl[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+            wl[6] = pc_iter;
+            wl[7] = n_refill;
+        }
+    }
     if (lane == 0) {
         if (!t_drain) t_drain = t_end;
         atomicMin(&st[25], t_drain);                 // work counter ran out

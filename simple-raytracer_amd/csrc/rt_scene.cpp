@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "rt_accel.h"
 #include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_hip.h"
@@ -71,24 +72,14 @@ struct rt_scene {
     long long opt_bvh_node = 500;      // DP collapse: cost of a 4-wide node visit, x1000 of a sphere test
                                        // (A/B, C3: 0.25 / 0.5 / 0.75 / 1 / 2 -> +0.6 / +0.5 / +0.5 / +0.2 / -1.7 %)
     long long opt_fail_bvh_upload = 0; // test hook: the next BVH uploads fail (RT_E_NOMEM)
-    // BVH inputs kept on the host (the boxes' padding depends on the eye)
-    struct PrimSrc {
-        int key;
-        bool sphere;
-        float lo[3], hi[3];            // face: vertex bounds; sphere: centre +- r
-        float c[3], r;                 // sphere centre / radius
-        double cond;                   // face: |e1|^2 |e2|^2 / det
-    };
-    std::vector<PrimSrc> prims;
-    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
+    AccelInput in;                     // host arrays + BVH sources (rt_accel.h)
+    long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
     float4 *d_leafrec = nullptr;
     DirK *d_dirk = nullptr;            // per light: shadow-region tree (directional lights)
     int *d_objleaf = nullptr;          // per object: its leaf's link in the main tree
-    std::vector<float4> h_fscan, h_sscan;   // host copies for the leaf records
-    std::vector<float> h_ofac;
-    std::vector<LightK> h_lights;
+    AccelTree last_tree_ms;            // phase times of the last build (bvh_phase_ms)
 
     int bvh_depth = 0;
     int bvh_stack = 0;
@@ -118,7 +109,6 @@ int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
     return RT_OK;
 }
 
-V3 f3(const float *p) { return {p[0], p[1], p[2]}; }
 
 // Dynamic LDS of render_kernel: the per-lane shading state, the mode's region
 // (BVH stacks or the staged primitives), then the lights when they all fit
@@ -202,262 +192,22 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     return render_launch(maxf, mode, pl, (unsigned)grid, shm, st);
 }
 
-// Distance bound for the BVH padding: from any ray origin (the eye, or a point
-// inside the scene's bounds) to any primitive.
-double distance_bound(const rt_scene *s, const float eye[3]) {
-    double diag2 = 0, far2 = 0, mag = 0;
-    for (int k = 0; k < 3; k++) {
-        double e = s->scene_hi[k] - s->scene_lo[k];
-        diag2 += e * e;
-        double a = std::fabs(eye[k] - s->scene_lo[k]), b = std::fabs(eye[k] - s->scene_hi[k]);
-        far2 += std::max(a, b) * std::max(a, b);
-        mag = std::max(mag, std::max(std::fabs((double)s->scene_lo[k]), std::fabs((double)s->scene_hi[k])));
-        mag = std::max(mag, std::fabs((double)eye[k]));
-    }
-    return std::max(std::sqrt(diag2), std::sqrt(far2)) + mag + 1.0;
-}
-
-// Binary SAH tree over P, collapsed into 4-wide nodes (opt_bvh_collapse: 0
-// greedy, largest child area first; 1 SAH-optimal) and renumbered breadth-first
-// (the top levels first: cache locality of the hot nodes).
-bool build_wide(rt_scene *s, std::vector<rtbvh::Prim> &P, rtbvh::Result &R, rtbvh::Result4 &Q) {
-    rtbvh::Builder B(P);
-    B.max_leaf = s->opt_bvh_collapse ? 1 : (int)s->opt_bvh_leaf;
-    B.trav_cost = 0.5f;                // SAH node cost, in sphere tests (A/B over 0.25-2: 0.5 best, round 1)
-    if (!B.build(R) || R.nodes.empty()) return false;
-    if (s->opt_bvh_collapse)
-        rtbvh::collapse_sah<4>(R, Q, (int)s->opt_bvh_leaf, (float)s->opt_bvh_node / 1000.0f);
-    else
-        rtbvh::collapse<4>(R, Q);
-    rtbvh::bfs_order(Q);
-    return true;
-}
-
-// Shadow-cone tree of a directional light (Params::dirk, dir_bf == 2).
-//
-// The reference's directional shadow ray runs TraceRay with the light's
-// UNNORMALISED direction d = -dir (main.cpp:895), and the sphere test
-// assumes |d| = 1 (main.cpp:1225-1258).  With s = |d|, n = d / s, k = s^2 - 1,
-// h = n.(c - o) (how far the centre is ahead of the origin along the ray) and
-// l = the lateral distance of c from the ray's line, the discriminant is
-//     det / 4 = (d.w)^2 - |w|^2 + r^2 = k h^2 - l^2 + r^2,
-// and the sphere shadows o iff det >= 0 and its far root (-B + sqrt det) / 2
-// exceeds epsilon: for h < 0 that needs o inside the sphere; for h >= 0 it is
-// l^2 <= r^2 + k h^2 -- a cylinder (s = 1), a cone widening away from the
-// light (s > 1) or a bounded cap (s < 1).  It is NOT a ray-geometry
-// question, so the ray BVH cannot cull it.  Here the spheres get a tree of
-// their own, built in the frame whose z axis is n (rows of R: u1, u2, n) over
-// boxes c' +- r_e, and a shadow ray becomes a cone query from R o (device:
-// bvh_trace<true>): a child is entered iff its top is not below the origin
-// (tz >= 0), its lateral distance d from the origin satisfies
-// d^2 <= max(0, k) tz^2, and for s < 1 its bottom is within
-// r_e / sqrt(1 - s^2).  Every candidate is then tested with the exact
-// reference arithmetic; the tree only decides which spheres are tested.
-// Conservative margins: the computed discriminant's error, up to ~2^-21
-// (1 + s^2) D^2, grows r^2 by 2^-18 (1 + s^2) D^2 (r_e), boxes grow by 2^-16 D,
-// k is rounded up.  Returns false if the direction or the geometry is not
-// finite, or the scene is so large that one ulp of B reaches epsilon (then
-// the h < 0 side is no longer safe): the caller falls back to the scan.
-bool dir_tree(rt_scene *s, const LightK &lt, double D, std::vector<rtbvh::Node4H> &nodes, std::vector<float4> &rec,
-              DirK &out, int &max_stack) {
-    for (int k = 0; k < 9; k++) out.R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
-    out.root = -1;
-    out.cone_k = 0.0f;
-    out.cone_h = INFINITY;
-    const double dx = lt.sdir[0], dy = lt.sdir[1], dz = lt.sdir[2];
-    const double sl = std::sqrt(dx * dx + dy * dy + dz * dz);
-    if (!std::isfinite(sl) || !(sl > 0.0)) return false;
-    if (std::ldexp(2.0 * sl * D, -23) >= 0.5 * (double)s->base.eps) return false;
-    const double n[3] = {dx / sl, dy / sl, dz / sl};
-    // u1 perpendicular to n (cross with the axis least aligned with n), u2 = n x u1
-    int ax = 0;
-    for (int k = 1; k < 3; k++)
-        if (std::fabs(n[k]) < std::fabs(n[ax])) ax = k;
-    double e[3] = {0, 0, 0};
-    e[ax] = 1.0;
-    double u1[3] = {n[1] * e[2] - n[2] * e[1], n[2] * e[0] - n[0] * e[2], n[0] * e[1] - n[1] * e[0]};
-    const double l1 = std::sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
-    for (double &v : u1) v /= l1;
-    const double u2[3] = {n[1] * u1[2] - n[2] * u1[1], n[2] * u1[0] - n[0] * u1[2], n[0] * u1[1] - n[1] * u1[0]};
-    for (int k = 0; k < 3; k++) {
-        out.R[k] = (float)u1[k];
-        out.R[3 + k] = (float)u2[k];
-        out.R[6 + k] = (float)n[k];
-    }
-    // the device rotates with the float R: boxes are computed with it too
-    // (its rounding of R o, ~2^-22 D, is far inside the 2^-16 D margins)
-    double R[9];
-    for (int k = 0; k < 9; k++) R[k] = out.R[k];
-    const double pad = std::ldexp(D, -16);
-    const double s2 = sl * sl;
-    std::vector<rtbvh::Prim> P;
-    double re_max = 0.0;
-    for (const auto &src : s->prims) {
-        if (!src.sphere) continue;
-        const double c[3] = {src.c[0], src.c[1], src.c[2]};
-        const double r = std::fabs((double)src.r);
-        if (!std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]) || !std::isfinite(r)) return false;
-        const double re = std::sqrt(r * r + std::ldexp((1.0 + s2) * D * D, -18)) + 2.0 * pad;
-        re_max = std::max(re_max, re);
-        rtbvh::Prim q;
-        q.key = src.key;
-        q.cost = 1.0f;
-        for (int k = 0; k < 3; k++) {
-            const double cr = R[3 * k] * c[0] + R[3 * k + 1] * c[1] + R[3 * k + 2] * c[2];
-            q.box.lo[k] = std::nextafter((float)(cr - re), -INFINITY);
-            q.box.hi[k] = std::nextafter((float)(cr + re), INFINITY);
-            q.c[k] = (float)cr;
-        }
-        P.push_back(q);
-    }
-    if (P.empty()) return true;                          // root -1: no sphere can shadow
-    out.cone_k = std::nextafter((float)(std::max(0.0, s2 - 1.0) * (1.0 + std::ldexp(1.0, -16))), INFINITY);
-    if (s2 < 1.0) out.cone_h = std::nextafter((float)(re_max / std::sqrt(1.0 - s2) + pad), INFINITY);
-    rtbvh::Result Rb;
-    rtbvh::Result4 Q;
-    if (!build_wide(s, P, Rb, Q) || Q.max_stack > kStackMax) return false;
-    max_stack = Q.max_stack;
-    const int nf = s->base.nf;
-    bool ok = rtbvh::leaf_records(
-        Q, Rb.keys, [](int32_t) { return false; },
-        [&](int32_t k) {
-            float kb;
-            memcpy(&kb, &k, sizeof kb);
-            rec.push_back(s->h_sscan[k - nf]);
-            rec.push_back(make_float4(kb, s->h_ofac[k], 0.0f, 0.0f));
-            return 2;
-        },
-        rec.size());
-    std::vector<rtbvh::Node4H> QQ;
-    if (!ok || !rtbvh::quantize(Q, QQ)) return false;
-    const int base = (int)nodes.size();
-    for (auto &z : QQ) {
-        for (auto &l : z.link) {
-            if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
-            else if (l >= 0) l += base;
-        }
-        nodes.push_back(z);
-    }
-    out.root = base;
-    return true;
-}
-
-// (Re)build the BVH with boxes padded for distance bound D (see rt_bvh.h):
-//   face   pad = 2^-16 * D * max(1, cond)                 (32x the rounding bound)
-//   sphere radius' = sqrt(r^2 + 2^-18 D^2) + 2^-16 D     (discriminant error)
+// (Re)build the BVH for distance bound D on the host (rt_accel.cpp) and
+// upload it.
 int build_bvh(rt_scene *s, double D) {
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<rtbvh::Prim> P(s->prims.size());
-    for (size_t i = 0; i < P.size(); i++) {
-        const auto &src = s->prims[i];
-        rtbvh::Prim &q = P[i];
-        q.key = src.key;
-        if (!src.sphere) {
-            double pad = std::ldexp(D, -16) * std::max(1.0, src.cond);
-            for (int k = 0; k < 3; k++) {
-                q.box.lo[k] = (float)(src.lo[k] - pad);
-                q.box.hi[k] = (float)(src.hi[k] + pad);
-                q.c[k] = 0.5f * (src.lo[k] + src.hi[k]);
-            }
-            q.cost = 3.0f;
-        } else {
-            double r = std::fabs((double)src.r);
-            double rr = std::sqrt(r * r + std::ldexp(D * D, -18)) + std::ldexp(D, -16);
-            for (int k = 0; k < 3; k++) {
-                q.box.lo[k] = (float)(src.c[k] - rr);
-                q.box.hi[k] = (float)(src.c[k] + rr);
-                q.c[k] = src.c[k];
-            }
-            q.cost = 1.0f;
-        }
-        // float rounding of the padded box must not shrink it
-        for (int k = 0; k < 3; k++) {
-            q.box.lo[k] = std::nextafter(q.box.lo[k], -INFINITY);
-            q.box.hi[k] = std::nextafter(q.box.hi[k], INFINITY);
-            if (!std::isfinite(q.box.lo[k]) || !std::isfinite(q.box.hi[k])) {
-                q.box.lo[k] = -INFINITY;   // NaN/inf geometry: a box every ray enters
-                q.box.hi[k] = INFINITY;
-            }
-        }
-    }
-    rtbvh::Result R;
-    rtbvh::Result4 Q;
-    bool ok = P.empty() || build_wide(s, P, R, Q);
-    // leaf records: face = its 5 scan words with (key, shadow factor) in the
-    // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
-    std::vector<float4> rec;
-    const int nf = s->base.nf;
-    if (ok && !Q.nodes.empty())
-        ok = rtbvh::leaf_records(Q, R.keys, [nf](int32_t k) { return k < nf; }, [&](int32_t k) {
-            float kb;
-            memcpy(&kb, &k, sizeof kb);
-            float fac = s->h_ofac[k];
-            if (k < nf) {
-                for (int j = 0; j < 5; j++) rec.push_back(s->h_fscan[5 * (size_t)k + j]);
-                rec.back().y = kb;
-                rec.back().z = fac;
-                return 5;
-            }
-            rec.push_back(s->h_sscan[k - nf]);
-            rec.push_back(make_float4(kb, fac, 0.0f, 0.0f));
-            return 2;
-        });
-    rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));   // 5-word reads of a last sphere
-    // every object's leaf in the main tree (the origin-leaf pass, bvh_trace)
-    std::vector<int32_t> objleaf((size_t)std::max(1, nf + s->base.ns), rtbvh::kEmptyLeaf);
-    if (ok)
-        for (const auto &n : Q.nodes)
-            for (int32_t l : n.link) {
-                if (l >= 0 || l == rtbvh::kEmpty) continue;
-                const int v = -l - 1, nfc = (v >> 4) & 15, count = v & 15;
-                size_t off = (size_t)(v >> 8);
-                for (int k = 0; k < count; k++) {
-                    int32_t key;
-                    if (k < nfc) {
-                        memcpy(&key, &rec[off + 4].y, sizeof key);
-                        off += 5;
-                    } else {
-                        memcpy(&key, &rec[off + 1].x, sizeof key);
-                        off += 2;
-                    }
-                    objleaf[(size_t)key] = l;
-                }
-            }
-    std::vector<rtbvh::Node4H> QQ;
-    if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ)) ok = false;     // non-finite geometry: scan
-    for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
-        for (auto &l : z.link)
-            if (l == rtbvh::kEmpty) l = rtbvh::kEmptyLeaf;
-    // the spill area is sized for the deepest tree (kStackMax: far beyond any
-    // tree the builder's depth cap allows)
-    ok = ok && !Q.nodes.empty() && Q.max_stack <= kStackMax;
-    // directional lights in a scene with spheres: shadow-region trees, after
-    // the main tree in the same node and record arrays
-    std::vector<DirK> dirk(s->h_lights.size());
-    int dir_mode = 0;
-    int stack_all = Q.max_stack;                 // deepest stack over the main and the cone trees
-    if (ok && s->base.ns > 0) {
-        rec.resize(rec.size() - 3);                  // the 3 padding words go after the last tree
-        for (size_t l = 0; l < s->h_lights.size(); l++) {
-            if (s->h_lights[l].w != 0.0f) continue;
-            if (dir_mode == 0) dir_mode = 2;
-            int st = 0;
-            if (!dir_tree(s, s->h_lights[l], D, QQ, rec, dirk[l], st)) dir_mode = 1;
-            stack_all = std::max(stack_all, st);
-        }
-        rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    }
-    // device links: an inner node's link is its byte offset in the node array
-    // (the kernel fetches a node with buffer loads at that offset: no address
-    // arithmetic per visit), leaf links stay as they are
-    if (ok && QQ.size() * sizeof(rtbvh::Node4H) > (size_t)INT32_MAX) ok = false;
-    if (ok) {
-        for (auto &z : QQ)
-            for (auto &l : z.link)
-                if (l >= 0) l *= (int32_t)sizeof(rtbvh::Node4H);
-        for (auto &d : dirk)
-            if (d.root >= 0) d.root *= (int)sizeof(rtbvh::Node4H);
-    }
+    AccelOpts o;
+    o.bvh_leaf = (int)s->opt_bvh_leaf;
+    o.collapse = (int)s->opt_bvh_collapse;
+    o.node_milli = (int)s->opt_bvh_node;
+    o.threads = (int)s->opt_bvh_threads;
+    AccelTree T;
+    build_accel(s->in, D, o, T);
+    bool ok = T.ok;
+    const std::vector<rtbvh::Node4H> &QQ = T.nodes;
+    const std::vector<float4> &rec = T.rec;
+    const std::vector<DirK> &dirk = T.dirk;
+    const std::vector<int32_t> &objleaf = T.objleaf;
     // The old tree stays valid until the new one is on the device: upload into
     // new buffers first, then swap (a failed rebuild leaves no dangling
     // pointers and no tree marked valid that is not there).
@@ -508,14 +258,17 @@ int build_bvh(rt_scene *s, double D) {
     s->base.bvh = nb;
     s->base.leafrec = nr;
     s->base.dirk = nd;
-    s->base.dir_bf = dir_mode;
+    s->base.dir_bf = T.dir_mode;
     s->bvh_ok = ok && rc == RT_OK;
     s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
-    s->bvh_depth = s->bvh_ok ? Q.depth : 0;
-    s->bvh_stack = s->bvh_ok ? Q.max_stack : 0;
+    s->bvh_depth = s->bvh_ok ? T.depth : 0;
+    s->bvh_stack = s->bvh_ok ? T.max_stack : 0;
     // spill area per lane: every block of kSpill entries a stack can push out
-    s->ovf_stride = s->bvh_ok ? (stack_all / kSpill + 1) * kSpill : kSpill;
-    s->bvh_nodes = s->bvh_ok ? (long long)Q.nodes.size() : 0;
+    s->ovf_stride = s->bvh_ok ? (T.stack_all / kSpill + 1) * kSpill : kSpill;
+    s->bvh_nodes = s->bvh_ok ? T.main_nodes : 0;
+    s->last_tree_ms = AccelTree();
+    for (int k = 0; k < 6; k++) s->last_tree_ms.ms[k] = T.ms[k];
+    s->last_tree_ms.threads = T.threads;
     s->bvh_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return rc;
 }
@@ -527,7 +280,7 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
     bool bvh = s->opt_accel == 1 || (s->opt_accel == -1 && nobj > 32);
     int mode = MODE_SCAN;
     if (bvh) {
-        double D = distance_bound(s, p.eye);
+        double D = distance_bound(s->in, p.eye);
         if (D > s->bvh_D) {
             int rc = build_bvh(s, std::max(D, 1.5 * s->bvh_D));
             if (rc) return rc;
@@ -575,7 +328,7 @@ void free_slot(RenderSlot &r) {
 // packets of caller (or collective) streams that share a hardware queue.
 int init_slot(RenderSlot &r, bool own_stream) {
     if (hipMalloc(&r.work, sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
-    if (hipMalloc(&r.stats, kNStats * sizeof(unsigned long long)) != hipSuccess) return RT_E_NOMEM;
+    if (hipMalloc(&r.stats, kStatsAlloc * sizeof(unsigned long long)) != hipSuccess) return RT_E_NOMEM;
     if (hipEventCreate(&r.ev0) != hipSuccess || hipEventCreate(&r.ev1) != hipSuccess ||
         hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming) != hipSuccess)
         return RT_E_HIP;
@@ -689,117 +442,22 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
 
     auto *s = new rt_scene();
     s->device = device;
-    const int nf = desc->n_faces, ns = desc->n_spheres, nobj = nf + ns;
+    const int nf = desc->n_faces, ns = desc->n_spheres;
 
-    // --- faces: exact per-face invariants (TraceRay recomputes these per call)
-    std::vector<float4> fscan((size_t)nf * 5);
-    std::vector<FaceShadeK> fsh((size_t)nf);
-    std::vector<ObjK> objs((size_t)nobj);
-    std::vector<float> ofac((size_t)nobj);
-    auto fill_obj = [&](int k, const rt_material &m, int tex, int is_sphere) {
-        ObjK &o = objs[k];
-        for (int c = 0; c < 3; c++) o.dif[c] = m.diffuse[c], o.spc[c] = m.specular[c];
-        o.ka = m.ka, o.kd = m.kd, o.ks = m.ks, o.n = m.n, o.opacity = m.opacity, o.eta = m.eta;
-        o.tex = tex;
-        o.is_sphere = is_sphere;
-        ofac[k] = (float)(1.0 - (double)m.opacity);
-        if (m.ks > 0.0f || (m.opacity < 1.0f && m.eta > 0.0f)) s->secondary = true;
-    };
-    for (int i = 0; i < nf; i++) {
-        const rt_face_desc &F = desc->faces[i];
-        V3 v0 = f3(F.v[0]), v1 = f3(F.v[1]), v2 = f3(F.v[2]);
-        V3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
-        V3 n = vnorm(vcross(e1, e2));                         // main.cpp:537-539
-        float D = -vdot(n, v0);
-        float d11 = vdot(e1, e1), d12 = vdot(e1, e2), d22 = vdot(e2, e2);
-        float det = (d11 * d22 - d12 * d12);
-        fscan[5 * i + 0] = make_float4(v0.x, v0.y, v0.z, D);
-        fscan[5 * i + 1] = make_float4(n.x, n.y, n.z, det);
-        fscan[5 * i + 2] = make_float4(e1.x, e1.y, e1.z, d11);
-        fscan[5 * i + 3] = make_float4(e2.x, e2.y, e2.z, d22);
-        fscan[5 * i + 4] = make_float4(d12, 0.0f, 0.0f, 0.0f);
-        FaceShadeK &fs = fsh[i];
-        for (int k = 0; k < 3; k++) {
-            V3 vn = vnorm(f3(F.vn[k]));
-            fs.vn[k][0] = vn.x, fs.vn[k][1] = vn.y, fs.vn[k][2] = vn.z;
-            for (int c = 0; c < 2; c++) {
-                float t = F.vt[k][c];
-                fs.vt[k][c] = (t < 0.0f) ? 0.0f : ((1.0f < t) ? 1.0f : t);
-            }
-        }
-        fs.smooth = F.smooth;
-        fill_obj(i, F.mat, F.texture, 0);
-    }
-    // BVH sources (padding is applied per build, it depends on the eye)
-    s->prims.reserve((size_t)nobj);
-    for (int i = 0; i < nf; i++) {
-        rt_scene::PrimSrc ps{};
-        ps.key = i;
-        ps.sphere = false;
-        const rt_face_desc &F = desc->faces[i];
-        for (int k = 0; k < 3; k++) {
-            ps.lo[k] = std::min(F.v[0][k], std::min(F.v[1][k], F.v[2][k]));
-            ps.hi[k] = std::max(F.v[0][k], std::max(F.v[1][k], F.v[2][k]));
-        }
-        float4 a = fscan[5 * i + 1], b2 = fscan[5 * i + 2], c2 = fscan[5 * i + 3];
-        double det = a.w, d11 = b2.w, d22 = c2.w;
-        ps.cond = det > 0 ? d11 * d22 / det : 1e30;
-        s->prims.push_back(ps);
-    }
-    std::vector<float4> sscan((size_t)ns);
-    for (int i = 0; i < ns; i++) {
-        const rt_sphere_desc &S = desc->spheres[i];
-        sscan[i] = make_float4(S.center[0], S.center[1], S.center[2], S.radius);
-        fill_obj(nf + i, S.mat, S.texture, 1);
-        rt_scene::PrimSrc ps{};
-        ps.key = nf + i;
-        ps.sphere = true;
-        for (int k = 0; k < 3; k++) {
-            ps.c[k] = S.center[k];
-            ps.lo[k] = S.center[k] - std::fabs(S.radius);
-            ps.hi[k] = S.center[k] + std::fabs(S.radius);
-        }
-        ps.r = S.radius;
-        s->prims.push_back(ps);
-    }
-    for (int k = 0; k < 3; k++) s->scene_lo[k] = INFINITY, s->scene_hi[k] = -INFINITY;
-    for (const auto &ps : s->prims)
-        for (int k = 0; k < 3; k++) {
-            if (std::isfinite(ps.lo[k])) s->scene_lo[k] = std::min(s->scene_lo[k], ps.lo[k]);
-            if (std::isfinite(ps.hi[k])) s->scene_hi[k] = std::max(s->scene_hi[k], ps.hi[k]);
-        }
-    for (int k = 0; k < 3; k++)
-        if (!(s->scene_lo[k] <= s->scene_hi[k])) s->scene_lo[k] = s->scene_hi[k] = 0.0f;
-    bool nan_fac = false;
-    for (float f : ofac) nan_fac |= std::isnan(f);
-    s->h_fscan = fscan;
-    s->h_sscan = sscan;
-    s->h_ofac = ofac;
-    s->h_lights.clear();
-    std::vector<LightK> lights((size_t)desc->n_lights);
-    for (int i = 0; i < desc->n_lights; i++) {
-        const rt_light_desc &L = desc->lights[i];
-        LightK &k = lights[i];
-        memset(&k, 0, sizeof k);
-        for (int c = 0; c < 3; c++) k.xyz[c] = L.xyz[c], k.col[c] = L.color[c];
-        k.w = L.w;
-        V3 dir = f3(L.xyz);
-        V3 Ld = vmul(vnorm(dir), -1.0f);
-        V3 sd = vmul(dir, -1.0f);
-        k.L[0] = Ld.x, k.L[1] = Ld.y, k.L[2] = Ld.z;
-        k.sdir[0] = sd.x, k.sdir[1] = sd.y, k.sdir[2] = sd.z;
-    }
-    s->h_lights = lights;
+    // the per-object arrays and the BVH sources, on the host (rt_accel.cpp)
+    accel_input(desc, s->in);
+    const AccelInput &in = s->in;
+    s->secondary = in.secondary;
     std::vector<TexK> texs((size_t)desc->n_textures);
 
     int rc = RT_OK;
     Params &p = s->base;
-    if (!rc) rc = upload(s, fscan, p.fscan);
-    if (!rc) rc = upload(s, sscan, p.sscan);
-    if (!rc) rc = upload(s, ofac, p.ofac);
-    if (!rc) rc = upload(s, objs, p.objs);
-    if (!rc) rc = upload(s, fsh, p.fsh);
-    if (!rc) rc = upload(s, lights, p.lights);
+    if (!rc) rc = upload(s, in.fscan, p.fscan);
+    if (!rc) rc = upload(s, in.sscan, p.sscan);
+    if (!rc) rc = upload(s, in.ofac, p.ofac);
+    if (!rc) rc = upload(s, in.objs, p.objs);
+    if (!rc) rc = upload(s, in.fsh, p.fsh);
+    if (!rc) rc = upload(s, in.lights, p.lights);
     std::vector<unsigned char> texels;
     for (int i = 0; i < desc->n_textures; i++) {
         const rt_texture_desc &T = desc->textures[i];
@@ -833,32 +491,17 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.eps = desc->epsilon;
     p.depth = desc->depth;
     p.dir_bf = 0;                      // set with the BVH (build_bvh); the scan needs none
-    p.shadow_early_out = nan_fac ? 0 : 1;
+    p.shadow_early_out = in.nan_fac ? 0 : 1;
     p.chunk = 0;                       // launch_one: chunk_for, refill_for
     p.refill_min = 1;
     p.gate_x = kGateX;
     // The origin-leaf pass for reflection and refraction rays pays in dense
     // scenes (C5: +2.3 %) and costs sparse ones (C3: -1.1 %;
-    // profiles/r03/ab_origin_leaf.txt).  Density here: the objects a straight
-    // line across the scene's box meets on average -- total cross-section
-    // (spheres pi r^2, triangles area / 2, averaged over directions) per
-    // volume, times the box diagonal (C3: ~3, C5: ~200).
-    {
-        double xs = 0.0, vol = 1.0, diag2 = 0.0;
-        for (int i = 0; i < nf; i++) {
-            V3 c = vcross(f3(&fscan[5 * i + 2].x), f3(&fscan[5 * i + 3].x));
-            xs += 0.25 * std::sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z);
-        }
-        for (int i = 0; i < ns; i++) xs += kPi * (double)sscan[i].w * (double)sscan[i].w;
-        for (int k = 0; k < 3; k++) {
-            const double e = (double)s->scene_hi[k] - (double)s->scene_lo[k];
-            vol *= e;
-            diag2 += e * e;
-        }
-        s->crossings = vol > 0.0 && std::isfinite(xs) ? xs / vol * std::sqrt(diag2) : 0.0;
-        s->org_first_auto = s->crossings > kOrgDensity ? kOrgFirst : 0;
-        p.org_first = s->org_first_auto;
-    }
+    // profiles/r03/ab_origin_leaf.txt); the density is AccelInput::crossings
+    // (C3: ~3, C5: ~200).
+    s->crossings = in.crossings;
+    s->org_first_auto = s->crossings > kOrgDensity ? kOrgFirst : 0;
+    p.org_first = s->org_first_auto;
     s->lds_bytes = (size_t)(5 * nf + ns) * sizeof(float4);
     *out = s;
     return RT_OK;
@@ -914,9 +557,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         if (value < kSpill + 4 || value > kLdsStack) return RT_E_INVALID;
         s->opt_lds_stack = value;
     }
-    else if (k == "bvh_leaf" || k == "bvh_collapse" || k == "bvh_node") {
+    else if (k == "bvh_leaf" || k == "bvh_collapse" || k == "bvh_node" || k == "bvh_threads") {
         if (k == "bvh_leaf") s->opt_bvh_leaf = std::max(1LL, std::min(15LL, value));
         else if (k == "bvh_collapse") s->opt_bvh_collapse = value != 0;
+        else if (k == "bvh_threads") s->opt_bvh_threads = std::max(0LL, std::min(256LL, value));
         else s->opt_bvh_node = std::max(0LL, value);
         s->bvh_D = -1.0;               // rebuild on the next render
     }
@@ -1081,6 +725,20 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[43] = (unsigned long long)s->last_lights_in_lds;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
+}
+
+int rt_scene_debug_wavelog(rt_scene *s, unsigned long long *out, int n) {
+    if (kWaveLogMax == 0) return RT_E_INVALID;   // not an RT_PROF build
+    if (!s || !out || n < 0 || !s->last_valid) return RT_E_INVALID;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    const RenderSlot &slot = s->slots[(size_t)s->last_slot];
+    if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
+    const long long waves = std::min<long long>(s->last_grid * (kBlock / 64), kWaveLogMax);
+    const int words = (int)std::min<long long>(n, waves * kWaveLogWords);
+    if (words > 0 && hipMemcpy(out, slot.stats + kNStats, (size_t)words * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost) != hipSuccess)
+        return RT_E_HIP;
+    return words;
 }
 
 int rt_render_rows(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb, rt_stats *stats) {

@@ -90,7 +90,8 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
-               "rt_scene_set_option", "rt_scene_debug_counters", "rt_deinterleave_rows", "rt_strerror"]
+               "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_deinterleave_rows",
+               "rt_strerror"]
 
 
 def host_lib() -> C.CDLL:
@@ -152,6 +153,8 @@ def hip_lib() -> C.CDLL:
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_prepare.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+        if hasattr(L, "rt_scene_debug_wavelog"):   # absent from round-1..3 libraries (A/B baselines)
+            L.rt_scene_debug_wavelog.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
         if hasattr(L, "rt_deinterleave_rows"):
             L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                C.c_void_p, C.c_void_p]
@@ -350,6 +353,19 @@ class GpuScene:
             rc = hip_lib().rt_scene_debug_counters(self._h, buf, 32)
         _check(rc, "rt_scene_debug_counters")
         return list(buf)
+
+    def debug_wavelog(self, max_waves: int = 16384) -> list[list[int]] | None:
+        """Per-wave timeline of the last render (rt_scene_debug_wavelog; RT_PROF
+        builds only, else None): [start, prologue done, drained, end, HW_ID,
+        XCC_ID, iterations, refills] per wave."""
+        L = hip_lib()
+        if not hasattr(L, "rt_scene_debug_wavelog"):
+            return None
+        buf = (C.c_ulonglong * (8 * max_waves))()
+        n = L.rt_scene_debug_wavelog(self._h, buf, 8 * max_waves)
+        if n < 0:
+            return None
+        return [list(buf[i:i + 8]) for i in range(0, n, 8)]
 
 
 def render_scene(path: str, cwd: str | None = None, device: int = 0, depth: int | None = None,

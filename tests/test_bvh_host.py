@@ -43,3 +43,32 @@ def test_bvh_device_padding_stack(checker):
     assert r.returncode == 0 and r.stdout.startswith("spheres=800"), r.stdout + r.stderr
     stack = int(r.stdout.split("stack=")[1].split()[0])
     assert stack >= 24, r.stdout
+
+
+# Tree hashes (tools/bvh_bench.cpp: FNV-1a over the uploaded node, record,
+# object-leaf and cone-tree arrays) of the seeded benchmark scenes: the
+# round-3 builder's trees.  The round-4 builder (primitive array reordered in
+# place, one-pass range statistics, sparse bins for small ranges, subtrees on
+# threads, bitwise binary16 rounding) must build the same trees.
+BENCH_TREE_HASH = {"C3": "d0d4c36f4057bc62", "C4": "5023c92e900cccd1", "C5": "0fa041b2ecb60269"}
+
+
+@pytest.fixture(scope="module")
+def bvh_bench():
+    pkg = os.path.join(ROOT, "simple-raytracer_amd")
+    subprocess.run(["make", "-C", pkg, "bvh_bench"], check=True, stdout=subprocess.DEVNULL)
+    return os.path.join(pkg, "lib", "bvh_bench")
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
+def test_bvh_build_threads_identical(bvh_bench, tmp_path, cfg):
+    """The host build on 4 threads gives the serial build's trees bit for bit,
+    and both are the pinned trees of the seeded scene (no GPU)."""
+    import json
+    from rtamd import scenes as gen
+    path = gen.write_scene(str(tmp_path), cfg)
+    r = subprocess.run([bvh_bench, path, "4", "1"], capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout + r.stderr
+    j = json.loads(r.stdout)
+    assert j["identical"] and j["ok"] == 1, j
+    assert j["hash"] == BENCH_TREE_HASH[cfg], j
