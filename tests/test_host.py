@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import rtamd
-from conftest import PKG, SCENES, golden_names
+from conftest import PKG, ROOT, SCENES, golden_names
 from oracle_py import OracleScene, ppm_bytes, quantize as oq
 
 NAMES = golden_names()
@@ -169,3 +169,43 @@ def test_cli_messages(tmp_path):
     assert r.returncode != 0
     assert "ERROR: Must define a 'mtlcolor'. Please verify." in r.stderr
     assert "ERROR: Command 'sphere' is undefined. Please verify input." in r.stderr
+
+
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "SimpleRayTracer")
+
+# Scenes on which the reference stops before rendering: an uncaught exception
+# (abort, main.cpp:114 for an empty token, :558-561 for the parser's
+# rethrows) or a missing required command (message, exit 0, main.cpp:574-602).
+# A missing texture file is left out: read_texture then uses uninitialised
+# width / height (src/utility.h:62, :113) -- undefined behaviour that here
+# either wrote an image or was killed allocating; the CLI reports an error.
+REF_ERROR_SCENES = {
+    "double_space": BASE.replace("eye 0 0 0", "eye  0 0 0"),
+    "sphere_before_mtlcolor": BASE + "sphere 0 0 -3 1\n",
+    "mtlcolor_3_args": BASE + "mtlcolor 1 1 1\n",
+    "hfov_not_a_number": BASE.replace("hfov 60", "hfov abc"),
+    "imsize_width_1": BASE.replace("imsize 8 8", "imsize 1 8"),
+    "light_3_args": BASE + "light 1 1 1\n",
+    **{f"missing_{k}": "\n".join(l for l in BASE.splitlines() if not l.startswith(k + " ")) + "\n"
+       for k in ("imsize", "eye", "viewdir", "updir", "hfov", "bkgcolor")},
+}
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="reference binary not built (oracle/Makefile ref)")
+@pytest.mark.parametrize("name", sorted(REF_ERROR_SCENES) + ["nifty_pattern", "no_args", "no_such_file"])
+def test_cli_error_behaviour_matches_reference_binary(tmp_path, name):
+    """The drop-in CLI and the real reference binary on scenes the reference
+    rejects: identical stdout, stderr and exit status (or abort signal).  No
+    GPU is touched: both stop in the parser."""
+    if name == "nifty_pattern":           # showcases/nifty_pattern.txt: 'eye  0.0' (double space)
+        p = os.path.join(SCENES, "nifty_pattern.txt")
+        args = [p]
+    elif name == "no_args":
+        args = []
+    elif name == "no_such_file":
+        args = [str(tmp_path / "nope.txt")]
+    else:
+        args = [_write(tmp_path, REF_ERROR_SCENES[name])]
+    ref = subprocess.run([REF_BIN] + args, capture_output=True, text=True, timeout=60, cwd=str(tmp_path))
+    got = subprocess.run([CLI] + args, capture_output=True, text=True, timeout=60, cwd=str(tmp_path))
+    assert (got.returncode, got.stdout, got.stderr) == (ref.returncode, ref.stdout, ref.stderr)
