@@ -23,6 +23,8 @@
 //     -- the reference's parser and writer with this repo's hot path; a GPU test
 //     compares its PPMs with the reference's.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -160,10 +162,16 @@ Mat3D create_view_window_and_ray_trace(Vector3 view_origin, Vector3 view_directi
     const int W = (int)res_w, H = (int)res_h;
     std::vector<float> rgb((size_t)W * H * 3);
     rt_scene *scene = nullptr;
+    rt_stats st{};
     int rc = rt_scene_create(0, &desc, &scene);
-    if (rc == RT_OK) rc = rt_render_rows(scene, &cam, W, H, 0, H, rgb.data(), nullptr);
+    if (rc == RT_OK) rc = rt_render_rows(scene, &cam, W, H, 0, H, rgb.data(), &st);
     rt_scene_destroy(scene);
     if (rc != RT_OK) throw std::runtime_error(std::string("rt_hip render failed: ") + rt_strerror(rc));
+    // RT_HIP_SEAM_STATS set: say that this seam ran, with the GPU's TraceRay
+    // counts (a test asserts them against the reference's own call counts)
+    if (std::getenv("RT_HIP_SEAM_STATS"))
+        std::fprintf(stderr, "rt_hip seam: %dx%d rays primary %llu shadow %llu refraction %llu reflection %llu\n", W, H,
+                     st.primary, st.shadow, st.refraction, st.reflection);
 
     // --- quantisation main.cpp:760-762 into the reference's image type
     std::vector<long long> q(rgb.size());

@@ -479,7 +479,8 @@ def test_reference_main_with_hip_seam(name, golden):
     shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
     out = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
     try:
-        r = subprocess.run([SEAM_EXE, tmp_name], cwd=SCENES, capture_output=True, text=True, timeout=300)
+        env = dict(os.environ, RT_HIP_SEAM_STATS="1")
+        r = subprocess.run([SEAM_EXE, tmp_name], cwd=SCENES, capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, r.stderr
         data = open(out, "rb").read()
     finally:
@@ -488,6 +489,15 @@ def test_reference_main_with_hip_seam(name, golden):
                 os.remove(p)
     g = golden[name]
     W, H = g["width"], g["height"]
+    # the binding itself says it ran (the reference's own CPU definition of
+    # the seam would write the same PPM): its GPU ray counts are the
+    # reference's TraceRay calls (gprof counts in the golden)
+    marks = [l for l in r.stderr.splitlines() if l.startswith("rt_hip seam: ")]
+    assert len(marks) == 1, r.stderr
+    f = marks[0].split()
+    assert f[2] == f"{W}x{H}", marks[0]
+    rays = {f[k]: int(f[k + 1]) for k in range(4, 12, 2)}
+    assert rays["primary"] == W * H and sum(rays.values()) == g["trace_calls"], (marks[0], g["trace_calls"])
     toks = data.split()
     assert toks[:4] == [b"P3", str(W).encode(), str(H).encode(), b"255"]
     mine = np.array([int(t) for t in toks[4:]], dtype=np.uint64).view(np.int64).reshape(H, W, 3)
@@ -704,15 +714,19 @@ def test_extreme_batching_deep_scene(opts):
     assert _counts(st) == cnt
 
 
-def test_origin_leaf_pass_bit_identical():
+def test_origin_leaf_pass_bit_identical(tmp_path):
     """Option org_first: a secondary ray first tests the BVH leaf of the object
     it starts on (a closest hit found there bounds the search, an opaque
     occluder there ends a shadow ray), then searches from the root.  Images
     and ray counts are bit for bit those without it, for every combination of
     ray kinds, on C3 (2000 objects, glass), C3G (glass triangles: SKIP_TRANS),
-    C5 (100 000 spheres, depth 8) and test7 (NaN pixels); the automatic
-    setting turns it on for C5's dense scene and off for C3."""
+    C3D (a directional light over spheres: cone queries), C5 (100 000
+    spheres, depth 8) and test7 (NaN pixels); the automatic setting turns it
+    on for C5's dense scene and off for the others."""
     cases = [("C3_64x64.txt", 4, SCENES), ("C5_8x8.txt", 8, SCENES), ("test7_s.txt", 4, SCENES)]
+    for cfg in ("C3G", "C3D"):
+        (tmp_path / f"{cfg}_40x32.txt").write_text(gen.scene_text(cfg, w=40, h=32))
+        cases.append((f"{cfg}_40x32.txt", 4, str(tmp_path)))
     for name, depth, cwd in cases:
         hs = rtamd.HostScene(name, cwd=cwd)
         hs.set_depth(depth)
