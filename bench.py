@@ -150,14 +150,30 @@ def host_cores() -> dict:
             "omp_num_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or 0)}
 
 
-def load_pmc_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+def lib_sha16() -> str:
+    """sha256 (first 16 hex) of the librt_hip.so this process loads."""
+    import hashlib
+    import rtamd
+    with open(os.path.join(rtamd.LIB_DIR, "librt_hip.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_pmc_traffic(config: str, lib: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py), only when it was
+    measured on this very library (its lib_sha16): (bytes or None, note)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get(config, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(config)
     except (OSError, ValueError):
-        return None
+        return None, "no profiles/pmc_traffic.json"
+    if not e:
+        return None, f"no PMC summary for {config}"
+    if e.get("lib_sha16") != lib:
+        return None, (f"the PMC summary ({e.get('source')}) was measured on librt_hip.so {e.get('lib_sha16')}, "
+                      f"this run loads {lib}: traffic not reported")
+    return e.get("hbm_bytes_per_launch"), f"PMC summary {e.get('source')} of this library"
 
 
 def main() -> None:
@@ -299,7 +315,8 @@ def main() -> None:
         alg_bytes = 12 * px + scene_bytes
         # PMC bytes were collected for a whole-image launch: only the N=1 line's
         # launch is that launch (a rank's strip at N>1 is not measured)
-        traffic = load_pmc_traffic(args.config) if world == 1 else None
+        lib = lib_sha16()
+        traffic, traffic_note = load_pmc_traffic(args.config, lib) if world == 1 else (None, "N = 1 only")
         cpu = cpu_port = None
         if args.cpu_baseline == "auto" and world == 1:
             def gpu_rays(p):
@@ -356,7 +373,8 @@ def main() -> None:
                                   "basis, which exceeds peak once the BVH skips ~98% of the tests "
                                   "(brute_force_equivalent)",
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "render_kernel",
+                         "traffic": traffic, "traffic_note": traffic_note, "lib_sha16": lib,
+                         "kernel": "render_kernel",
                          "kernel_ms": round(float(np.mean(kernel_ms)), 3),
                          "per_step": {"achieved": round(flops / (elapsed / args.steps) / 1e12, 3),
                                       "frac": round(flops / (elapsed / args.steps) / 1e12

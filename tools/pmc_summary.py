@@ -29,6 +29,10 @@ for f in sorted(glob.glob(os.path.join(base, "p*", "run_kernel_trace.csv"))):
             dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
 # every pass is its own run of the same render(s): mean duration per dispatch
 out = {"kernel": KERNEL, "per_render": per, "kernel_ns_mean": sum(dur) / max(1, len(dur)), "dispatches": len(dur)}
+# the library the passes ran (bench.py reports traffic only for this one)
+import hashlib
+_lib = os.path.join(os.environ.get("RTAMD_LIB_DIR") or os.path.join(ROOT, "simple-raytracer_amd", "lib"), "librt_hip.so")
+out["lib_sha16"] = hashlib.sha256(open(_lib, "rb").read()).hexdigest()[:16] if os.path.exists(_lib) else None
 g = lambda k: per.get(k, float("nan"))
 d = {}
 d["valu_inst_per_wave"] = g("SQ_INSTS_VALU") / g("SQ_WAVES")
