@@ -13,7 +13,10 @@
 // device over xGMI, a device-side de-interleave and one copy to the host --
 // opt-in until a multi-device node has run tests/test_gpu_parity.py::
 // test_cli_rccl_gather_multi_device), --float-out FILE (raw float32 H*W*3
-// framebuffer), --stats.
+// framebuffer), --stats, --stats-json FILE (the one-shot run's phases on
+// the host clock: parse, scene upload, BVH build, render, device->host copy,
+// quantise + P3 write; '-' = stderr).
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -33,6 +36,9 @@
 namespace {
 
 const int kRowBlock = 8;
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
 
 // One process, N devices: every device renders its row set (rth_row_set)
 // into HBM, one RCCL gather collects the N buffers on the first device, a
@@ -126,8 +132,10 @@ int main(int argc, char *argv[]) {
                   << std::endl;
         return 0;
     }
+    const auto t_start = Clock::now();
     int depth = -1, W = -1, H = -1, gpus = 1, device = 0;
     bool stats = false;
+    const char *stats_json = nullptr;
     std::string gather;
     const char *float_out = nullptr;
     for (int i = 2; i < argc; i++) {
@@ -139,10 +147,15 @@ int main(int argc, char *argv[]) {
         else if (a == "--float-out" && i + 1 < argc) float_out = argv[++i];
         else if (a == "--gather" && i + 1 < argc) gather = argv[++i];
         else if (a == "--stats") stats = true;
+        else if (a == "--stats-json" && i + 1 < argc) stats_json = argv[++i];
     }
+    // phases of the one-shot run (--stats-json), host clock
+    double ph_parse = 0, ph_create = 0, ph_bvh = 0, ph_render = 0, ph_d2h = 0, ph_write = 0;
+    auto t = Clock::now();
     rth_scene *hs = nullptr;
     std::vector<char> msg(1 << 16);
     int rc = rth_parse_file(argv[1], &hs, msg.data(), (int)msg.size());
+    ph_parse = ms_since(t);
     if (rc > 0) {
         std::cout << msg.data() << std::endl;
         return 0;
@@ -192,13 +205,35 @@ int main(int argc, char *argv[]) {
     // (device g gets blocks g, g+N, ...: every device the same mix of cheap
     // and costly rows), each renders its row set into a buffer of its own and
     // the blocks are put back in image order on the host.
-    for (int g = 0; g < gpus && gather == "host"; g++) {
+    // One device: each phase on its own, for --stats-json -- the scene upload,
+    // the BVH (rt_scene_prepare), the render into HBM, one device->host copy.
+    if (gather == "host" && gpus == 1) {
+        rt_scene *s = nullptr;
+        float *dimg = nullptr;
+        t = Clock::now();
+        int r = rt_scene_create(device, rth_desc(hs), &s);
+        ph_create = ms_since(t);
+        t = Clock::now();
+        if (!r) r = rt_scene_prepare(s, &cam, W, H);
+        ph_bvh = ms_since(t);
+        if (!r && hipMalloc(&dimg, img.size() * sizeof(float)) != hipSuccess) r = RT_E_NOMEM;
+        t = Clock::now();
+        if (!r) r = rt_render_rows(s, &cam, W, H, 0, H, dimg, &st[0]);
+        ph_render = ms_since(t);
+        t = Clock::now();
+        if (!r && hipMemcpy(img.data(), dimg, img.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+            r = RT_E_HIP;
+        ph_d2h = ms_since(t);
+        if (dimg) (void)hipFree(dimg);
+        rt_scene_destroy(s);
+        rcs[0] = r;
+    }
+    t = Clock::now();
+    for (int g = 0; g < gpus && gather == "host" && gpus > 1; g++) {
         pool.emplace_back([&, g] {
             rt_scene *s = nullptr;
             int r = rt_scene_create(device + g, rth_desc(hs), &s);
-            if (!r && gpus == 1) {
-                r = rt_render_rows(s, &cam, W, H, 0, H, img.data(), &st[g]);
-            } else if (!r) {
+            if (!r) {
                 std::vector<int> rows;
                 for (int b = g * kRowBlock; b < H; b += gpus * kRowBlock)
                     for (int y = b; y < std::min(H, b + kRowBlock); y++) rows.push_back(y);
@@ -215,7 +250,8 @@ int main(int argc, char *argv[]) {
             rcs[g] = r;
         });
     }
-    for (auto &t : pool) t.join();
+    for (auto &th : pool) th.join();
+    if (gpus > 1) ph_render = ms_since(t);      // scene, BVH, render and copies of every device
     for (int g = 0; g < gpus; g++) {
         if (rcs[g]) {
             std::cerr << "rt: render failed on device " << device + g << ": " << rt_strerror(rcs[g]) << std::endl;
@@ -241,10 +277,42 @@ int main(int argc, char *argv[]) {
     }
     char out[4096];
     rth_output_path(argv[1], out, sizeof out);
-    if (rth_write_ppm(out, img.data(), W, H, 0) != 0) {
+    t = Clock::now();
+    const int wr = rth_write_ppm(out, img.data(), W, H, 0);
+    ph_write = ms_since(t);
+    if (wr != 0) {
         std::cout << "ERROR: failed to create ppm image" << std::endl;
         return 0;
     }
     rth_free(hs);
+    if (stats_json) {
+        unsigned long long tot[4] = {0, 0, 0, 0};
+        double kms = 0, bvh_host = 0;
+        for (auto &s : st) {
+            tot[0] += s.primary, tot[1] += s.shadow, tot[2] += s.refraction, tot[3] += s.reflection;
+            kms = std::max(kms, s.kernel_ms);
+            bvh_host = std::max(bvh_host, s.bvh_build_ms);
+        }
+        long long ppm_bytes = 0;
+        if (FILE *f = fopen(out, "rb")) {
+            fseek(f, 0, SEEK_END);
+            ppm_bytes = ftell(f);
+            fclose(f);
+        }
+        const double total = ms_since(t_start);
+        const unsigned long long rays = tot[0] + tot[1] + tot[2] + tot[3];
+        FILE *f = std::strcmp(stats_json, "-") == 0 ? stderr : fopen(stats_json, "w");
+        if (f) {
+            fprintf(f,
+                    "{\"scene\": \"%s\", \"imsize\": [%d, %d], \"depth\": %d, \"gpus\": %d, \"gather\": \"%s\", "
+                    "\"rays\": %llu, \"phases_ms\": {\"parse\": %.3f, \"scene_upload\": %.3f, \"bvh_build\": %.3f, "
+                    "\"bvh_build_host\": %.3f, \"render\": %.3f, \"kernel\": %.3f, \"d2h\": %.3f, "
+                    "\"quantise_ppm_write\": %.3f}, \"total_ms\": %.3f, \"ppm_bytes\": %lld, "
+                    "\"Mrays_per_s_end_to_end\": %.3f, \"Mrays_per_s_kernel\": %.3f}\n",
+                    argv[1], W, H, depth, gpus, gather.c_str(), rays, ph_parse, ph_create, ph_bvh, bvh_host, ph_render,
+                    kms, ph_d2h, ph_write, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
+            if (f != stderr) fclose(f);
+        }
+    }
     return 0;
 }

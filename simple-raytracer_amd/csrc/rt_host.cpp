@@ -17,13 +17,21 @@
 // undefined behaviour; here that is reported like a stof failure.
 #include "rt_host.h"
 
+#include <fcntl.h>
+#include <sched.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -421,6 +429,19 @@ void copy_msg(char *msg, int msglen, const std::string &s) {
 }
 
 // main.cpp:760 on x86-64 (cvttss2si): NaN and out-of-range -> INT_MIN
+// Host threads for the writer: the process's CPU affinity, at most
+// OMP_NUM_THREADS when set (a GPU box's lease share) and 64.
+int host_threads() {
+    int n = 1;
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+        const int k = std::atoi(e);
+        if (k > 0) n = std::min(n, k);
+    }
+    return std::max(1, std::min(n, 64));
+}
+
 inline long long quantize1(float c) {
     float x = (c - 0.0f) * (255.0f - 0.0f) / (1.0f - 0.0f) + 0.0f;
     if (x >= -2147483648.0f && x < 2147483648.0f) return (long long)(int)x;
@@ -507,48 +528,103 @@ void rth_quantize(const float *rgb, long long n, long long *out) {
     for (long long i = 0; i < n; i++) out[i] = quantize1(rgb[i]);
 }
 
-// main.cpp:628-648: the std::to_string of each size_t, parallel formatting
+// main.cpp:628-648: "r g b \n" per pixel, each value the std::to_string of
+// the quantised size_t.  Host threads take chunks of pixels in order, format
+// each into a buffer of their own and write it with pwrite at its place in
+// the file: a chunk's offset is known once every earlier chunk has its length
+// (published in order, under a lock), so formatting and writing run on every
+// thread at once.  Values 0..255 (nearly all) come from a table; the rest
+// (background > 1, NaN's INT_MIN, negative values as size_t) through
+// std::to_chars.
 int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads) {
-    FILE *f = fopen(path, "wb");
-    if (!f) return -1;
-    fprintf(f, "P3 \n%d %d \n255 \n", W, H);
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return -1;
+    char head[64];
+    const int hn = std::snprintf(head, sizeof head, "P3 \n%d %d \n255 \n", W, H);
+    bool ok = ::pwrite(fd, head, (size_t)hn, 0) == (ssize_t)hn;
     const size_t npx = (size_t)W * (size_t)H;
-    if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
-    const size_t chunk = 1 << 16;
-    const size_t nchunks = (npx + chunk - 1) / chunk;
-    size_t next = 0;
-    int rc = 0;
-    while (next < nchunks) {
-        size_t batch = std::min(nchunks - next, (size_t)threads * 4);
-        std::vector<std::string> bufs(batch);
-        std::vector<std::thread> pool;
-        auto work = [&](size_t t0) {
-            for (size_t b = t0; b < batch; b += (size_t)threads) {
-                size_t p0 = (next + b) * chunk, p1 = std::min(npx, p0 + chunk);
-                std::string &s = bufs[b];
-                s.resize((p1 - p0) * 3 * 22);
-                char *o = s.data();
-                for (size_t p = p0; p < p1; p++) {
-                    for (int k = 0; k < 3; k++) {
-                        unsigned long long v = (unsigned long long)quantize1(rgb[p * 3 + k]);
-                        o = std::to_chars(o, o + 21, v).ptr;
-                        *o++ = ' ';
-                    }
-                    *o++ = '\n';
-                }
-                s.resize((size_t)(o - s.data()));
+    if (threads <= 0) threads = host_threads();
+    static const struct Lut {
+        char s[256][4];
+        unsigned char n[256];
+        Lut() {
+            for (int v = 0; v < 256; v++) {
+                char *o = std::to_chars(s[v], s[v] + 3, v).ptr;
+                n[v] = (unsigned char)(o - s[v] + 1);
+                *o = ' ';
             }
-        };
-        int nt = (int)std::min<size_t>((size_t)threads, batch);
-        for (int t = 1; t < nt; t++) pool.emplace_back(work, (size_t)t);
-        work(0);
-        for (auto &th : pool) th.join();
-        for (auto &s : bufs)
-            if (fwrite(s.data(), 1, s.size(), f) != s.size()) rc = -1;
-        next += batch;
-    }
-    if (fclose(f) != 0) rc = -1;
-    return rc;
+        }
+    } lut;
+    const size_t chunk = 1 << 15;
+    const size_t nchunks = (npx + chunk - 1) / chunk;
+    std::vector<size_t> len(nchunks, SIZE_MAX);       // formatted length of each chunk
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t next = 0;                                  // next chunk to take
+    size_t known = 0;                                 // chunks [0, known) have their offsets
+    size_t end_off = (size_t)hn;                      // file offset after chunk known - 1
+    std::vector<size_t> off(nchunks, 0);
+    auto format = [&](size_t c, std::string &o) {
+        const size_t p0 = c * chunk, p1 = std::min(npx, p0 + chunk);
+        o.resize((p1 - p0) * (3 * 21 + 1));
+        char *q = o.data();
+        for (size_t p = p0; p < p1; p++) {
+            for (int k = 0; k < 3; k++) {
+                const unsigned long long v = (unsigned long long)quantize1(rgb[p * 3 + k]);
+                if (v < 256) {
+                    std::memcpy(q, lut.s[v], 4);
+                    q += lut.n[v];
+                } else {
+                    q = std::to_chars(q, q + 20, v).ptr;
+                    *q++ = ' ';
+                }
+            }
+            *q++ = '\n';
+        }
+        o.resize((size_t)(q - o.data()));
+    };
+    std::atomic<bool> good{ok};
+    auto worker = [&] {
+        std::string buf;
+        for (;;) {
+            size_t c;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (next >= nchunks) return;
+                c = next++;
+            }
+            format(c, buf);
+            size_t at;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                len[c] = buf.size();
+                while (known < nchunks && len[known] != SIZE_MAX) {
+                    off[known] = end_off;
+                    end_off += len[known];
+                    known++;
+                }
+                cv.notify_all();
+                cv.wait(lk, [&] { return known > c; });
+                at = off[c];
+            }
+            size_t done = 0;
+            while (done < buf.size()) {
+                const ssize_t w = ::pwrite(fd, buf.data() + done, buf.size() - done, (off_t)(at + done));
+                if (w <= 0) {
+                    good = false;
+                    break;
+                }
+                done += (size_t)w;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    const int nt = (int)std::min<size_t>((size_t)threads, std::max<size_t>(1, nchunks));
+    for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+    worker();
+    for (auto &th : pool) th.join();
+    if (::close(fd) != 0) good = false;
+    return good ? 0 : -1;
 }
 
 int rth_output_path(const char *scene_path, char *out, int outlen) {
