@@ -25,6 +25,7 @@
 #include <atomic>
 #include <charconv>
 #include <climits>
+#include <cstdint>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -111,9 +112,14 @@ void load_p3(const std::string &path, int &w, int &h, std::vector<unsigned char>
     std::ifstream in(path, std::ios::binary);
     std::string data;
     if (in) {
-        std::ostringstream ss;
-        ss << in.rdbuf();
-        data = ss.str();
+        in.seekg(0, std::ios::end);
+        const std::streamoff size = in.tellg();
+        in.seekg(0, std::ios::beg);
+        if (size > 0) {
+            data.resize((size_t)size);
+            in.read(&data[0], size);
+            data.resize((size_t)in.gcount());
+        }
     } else {
         throw std::runtime_error("cannot open texture '" + path + "'");
     }
@@ -129,7 +135,24 @@ void load_p3(const std::string &path, int &w, int &h, std::vector<unsigned char>
             while (q < le) {
                 const char *t = q;
                 while (t < le && *t != ' ') t++;
-                if (t > q) {
+                if (t > q && ntok >= 4) {
+                    // a texel value: std::stoi, or a plain token of 1-9 digits
+                    // without it; values past the image are never converted
+                    // (the reference converts only w * h * 3 tokens,
+                    // src/utility.h:118-127)
+                    ntok++;
+                    if (got < need) {
+                        int v = 0;
+                        bool plain = t - q <= 9;
+                        for (const char *c = q; plain && c < t; c++) plain = *c >= '0' && *c <= '9';
+                        if (plain)
+                            for (const char *c = q; c < t; c++) v = v * 10 + (*c - '0');
+                        else
+                            v = std::stoi(std::string(q, t));
+                        rgb[got] = (unsigned char)std::clamp(v, 0, 255);
+                    }
+                    got++;
+                } else if (t > q) {
                     std::string tok(q, t);
                     ntok++;
                     if (ntok == 1) {
@@ -142,12 +165,8 @@ void load_p3(const std::string &path, int &w, int &h, std::vector<unsigned char>
                             need = (size_t)w * (size_t)h * 3;
                             rgb.assign(need, 0);
                         }
-                    } else if (ntok == 4) {
-                        if (tok != "255") throw std::invalid_argument("PPM pixel value must be between 0 - 255 .");
                     } else {
-                        int v = std::stoi(tok);
-                        if (got < need) rgb[got] = (unsigned char)std::clamp(v, 0, 255);
-                        got++;
+                        if (tok != "255") throw std::invalid_argument("PPM pixel value must be between 0 - 255 .");
                     }
                 }
                 q = t + 1;
@@ -158,9 +177,60 @@ void load_p3(const std::string &path, int &w, int &h, std::vector<unsigned char>
     if (w <= 0 || h <= 0 || got < need) throw std::out_of_range("vector::_M_range_check");
 }
 
+// std::stof of a plain decimal token ([-]digits[.digits], at most 15
+// significant digits -- what scene files hold) without strtof: M / 10^k with
+// M < 2^53 and k <= 22 is one correctly rounded double operation on exact
+// operands (Clinger's fast path), and rounding that double to float gives the
+// correctly rounded float -- strtof's result -- unless the double sits
+// exactly halfway between two floats (the true quotient may then lie on
+// either side): those, and every other token form (exponents, '+', hex,
+// inf / nan, prefixes like "1git", leading blanks), go to std::stof itself.
+float fast_stof(const std::string &s) {
+    static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    const char *p = s.data();
+    const size_t n = s.size();
+    size_t i = 0;
+    const bool neg = n > 0 && p[0] == '-';
+    if (neg) i = 1;
+    uint64_t m = 0;
+    int digits = 0, frac = 0;
+    bool dot = false, any = false;
+    for (; i < n; i++) {
+        const char c = p[i];
+        if (c >= '0' && c <= '9') {
+            any = true;
+            if (m == 0 && c == '0') {                     // leading zeros: no significant digit
+                if (dot) frac++;
+                continue;
+            }
+            if (++digits > 15) break;               // m < 10^15 < 2^53: exact in a double
+            m = m * 10 + (uint64_t)(c - '0');
+            if (dot) frac++;
+        } else if (c == '.' && !dot) {
+            dot = true;
+        } else {
+            break;
+        }
+    }
+    if (i == n && any && frac <= 22) {
+        double q = (double)m / kPow10[frac];              // exact operands: one rounding
+        uint64_t b;
+        std::memcpy(&b, &q, sizeof b);
+        const int e = (int)((b >> 52) & 0x7ff) - 1023;
+        // halfway between two normal floats: the 29 bits below float precision are 100...0
+        const bool tie = m != 0 && (b & ((uint64_t(1) << 29) - 1)) == (uint64_t(1) << 28);
+        if (!tie && (m == 0 || (e >= -126 && e <= 127))) {
+            const float f = (float)q;
+            return neg ? -f : f;
+        }
+    }
+    return std::stof(s);
+}
+
 float stof_or(const std::vector<std::string> &a, size_t i) {
     if (i >= a.size()) throw std::invalid_argument("stof");
-    return std::stof(a[i]);
+    return fast_stof(a[i]);
 }
 
 enum Cmd { EYE, VIEWDIR, UPDIR, HFOV, IMSIZE, BKGCOLOR, MTLCOLOR, TEXTURE, SPHERE, LIGHT, V, VN, VT, FACE };
@@ -302,20 +372,29 @@ struct Parser {
         S.faces.push_back(f);
     }
 
+    std::string name_;                       // this line's keyword token
+    std::vector<std::string> args_;          // and its arguments (storage reused line to line)
+
     void line(const std::string &text) {
         // tokenise exactly like main.cpp:107-117
-        std::vector<std::string> tok;
-        size_t pos = 0;
+        size_t pos = 0, ntok = 0;
         while (pos < text.size()) {
             size_t sp = text.find(' ', pos);
             if (sp == std::string::npos) sp = text.size();
             if (sp == pos) fail({}, "basic_string::at: __n (which is 0) >= this->size() (which is 0)", true);
-            tok.emplace_back(text, pos, sp - pos);
+            if (ntok == 0) {
+                name_.assign(text, pos, sp - pos);
+            } else {
+                if (args_.size() < ntok) args_.resize(ntok);
+                args_[ntok - 1].assign(text, pos, sp - pos);
+            }
+            ntok++;
             pos = sp + 1;
         }
-        if (tok.empty()) return;
-        const std::string name = tok.front();
-        std::vector<std::string> a(tok.begin() + 1, tok.end());
+        if (ntok == 0) return;
+        args_.resize(ntok - 1);
+        const std::string &name = name_;
+        const std::vector<std::string> &a = args_;
         Cmd c;
         if (a.empty() || !lookup(name, c)) return;
         try {
@@ -428,7 +507,6 @@ void copy_msg(char *msg, int msglen, const std::string &s) {
     msg[n] = 0;
 }
 
-// main.cpp:760 on x86-64 (cvttss2si): NaN and out-of-range -> INT_MIN
 // Host threads for the writer: the process's CPU affinity, at most
 // OMP_NUM_THREADS when set (a GPU box's lease share) and 64.
 int host_threads() {
@@ -442,6 +520,7 @@ int host_threads() {
     return std::max(1, std::min(n, 64));
 }
 
+// main.cpp:760 on x86-64 (cvttss2si): NaN and out-of-range -> INT_MIN
 inline long long quantize1(float c) {
     float x = (c - 0.0f) * (255.0f - 0.0f) / (1.0f - 0.0f) + 0.0f;
     if (x >= -2147483648.0f && x < 2147483648.0f) return (long long)(int)x;
