@@ -284,6 +284,7 @@ int main(int argc, char *argv[]) {
         std::cout << "ERROR: failed to create ppm image" << std::endl;
         return 0;
     }
+    const int eff_depth = rth_desc(hs)->depth;
     rth_free(hs);
     if (stats_json) {
         unsigned long long tot[4] = {0, 0, 0, 0};
@@ -309,7 +310,7 @@ int main(int argc, char *argv[]) {
                     "\"bvh_build_host\": %.3f, \"render\": %.3f, \"kernel\": %.3f, \"d2h\": %.3f, "
                     "\"quantise_ppm_write\": %.3f}, \"total_ms\": %.3f, \"ppm_bytes\": %lld, "
                     "\"Mrays_per_s_end_to_end\": %.3f, \"Mrays_per_s_kernel\": %.3f}\n",
-                    argv[1], W, H, depth, gpus, gather.c_str(), rays, ph_parse, ph_create, ph_bvh, bvh_host, ph_render,
+                    argv[1], W, H, eff_depth, gpus, gather.c_str(), rays, ph_parse, ph_create, ph_bvh, bvh_host, ph_render,
                     kms, ph_d2h, ph_write, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
             if (f != stderr) fclose(f);
         }
