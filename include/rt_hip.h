@@ -242,8 +242,9 @@ int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 /* Debug: the last render's per-wave timeline, RT_PROF builds only (others
  * return RT_E_INVALID).  8 words per wave of the launch: [0] wave start,
  * [1] prologue done, [2] work counter seen drained (0: never), [3] wave end
- * (100 MHz ticks, the clock of counters [24..29]), [4] HW_ID, [5] XCC_ID,
- * [6] outer iterations (trace steps), [7] refill batches.  Copies at most n
+ * (100 MHz ticks, the clock of counters [24..29]), [4] end of the wave's first
+ * trace step, [5] HW_ID << 32 | XCC_ID, [6] outer iterations (trace steps),
+ * [7] refill batches.  Copies at most n
  * words; returns the number copied. */
 int rt_scene_debug_wavelog(rt_scene *scene, unsigned long long *out, int n);
 

@@ -1461,6 +1461,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long t_drain = 0;
     unsigned long long n_refill = 0;
     const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_first = 0;      // end of the first trace step (its code fetched cold)
 #endif
     for (;;) {
 #if RT_PROF
@@ -1648,6 +1649,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_mixed += (__ballot(search && kind == RK_PRIMARY) != 0ull) && (__ballot(search && kind != RK_PRIMARY) != 0ull);
             unsigned long long c2 = __builtin_amdgcn_s_memtime();
             pc_trace += c2 - c1;
+            if (!t_first) t_first = __builtin_amdgcn_s_memrealtime();
 #endif
             bool need = search && q.bf;
             const unsigned long long nb = __ballot(need);
@@ -1701,8 +1703,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             wl[1] = t_loop;
             wl[2] = t_drain;
             wl[3] = t_end;
-            wl[4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-            wl[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+            wl[4] = t_first;
+            wl[5] = ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32) |   // HW_REG_HW_ID
+                    (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);                              // HW_REG_XCC_ID
             wl[6] = pc_iter;
             wl[7] = n_refill;
         }

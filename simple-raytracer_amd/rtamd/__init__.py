@@ -356,8 +356,8 @@ class GpuScene:
 
     def debug_wavelog(self, max_waves: int = 16384) -> list[list[int]] | None:
         """Per-wave timeline of the last render (rt_scene_debug_wavelog; RT_PROF
-        builds only, else None): [start, prologue done, drained, end, HW_ID,
-        XCC_ID, iterations, refills] per wave."""
+        builds only, else None): [start, prologue done, drained, end, first
+        trace step done, HW_ID << 32 | XCC_ID, iterations, refills] per wave."""
         L = hip_lib()
         if not hasattr(L, "rt_scene_debug_wavelog"):
             return None

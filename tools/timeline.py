@@ -86,6 +86,7 @@ def main():
     us = lambda t: (t - t0) / 100.0      # noqa: E731  (100 MHz ticks -> us)
     start = [us(w[0]) for w in wl]
     prologue = [(w[1] - w[0]) / 100.0 for w in wl]
+    first_step = [(w[4] - w[1]) / 100.0 for w in wl if w[4]]
     end = [us(w[3]) for w in wl]
     drained = [us(w[2]) for w in wl if w[2]]
     tail = [(w[3] - w[2]) / 100.0 for w in wl if w[2]]
@@ -101,7 +102,7 @@ def main():
         alive.append(sum(1 for s, e in zip(start, end) if s <= t < e))
     per_xcd = {}
     for w, s, e in zip(wl, start, end):
-        x = int(w[5]) & 0xF
+        x = int(w[5]) & 0xF           # XCC_ID
         per_xcd.setdefault(x, []).append((s, e, w[2] and us(w[2])))
     xcd = {str(x): {"waves": len(v), "start_p50": round(q([a for a, _, _ in v], 0.5), 2),
                     "start_max": round(max(a for a, _, _ in v), 2),
@@ -117,12 +118,14 @@ def main():
             "kernel": round(kernel_us, 2),
             "wave_start": summary(start),
             "prologue": summary(prologue),
+            "first_trace_step": summary(first_step) if first_step else None,
             "work_drained": summary(drained) if drained else None,
             "wave_tail_after_drain": summary(tail) if tail else None,
             "wave_end": summary(end),
             "wave_life": summary(life),
         },
         "iterations_per_wave": summary(iters),
+        "mean_step_us": round(sum((w[3] - w[4]) / 100.0 for w in wl if w[4]) / max(1, sum(max(0, w[6] - 1) for w in wl)), 3),
         "refills_per_wave": summary(refills),
         "alive_waves_by_twentieth": alive,
         "per_xcd": xcd,
