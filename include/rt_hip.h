@@ -239,6 +239,13 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * in LDS (1) or read from device memory (0).  n <= 48. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
+/* The last render's back() reads of an empty medium stack (main.cpp:1028,
+ * undefined behaviour in the reference; defined here as eta_bkg): writes the
+ * (x, y) image coordinates of the first min(events, n, 4096) events' pixels
+ * into xy[2k], xy[2k+1] (a pixel repeats once per event) and returns the
+ * number of events (rt_stats.ub_back), or a negative RT_E_* code. */
+int rt_scene_debug_ub_pixels(rt_scene *scene, int *xy, int n);
+
 /* Debug: the last render's per-wave timeline, RT_PROF builds only (others
  * return RT_E_INVALID).  8 words per wave of the launch: [0] wave start,
  * [1] prologue done, [2] work counter seen drained (0: never), [3] wave end

@@ -104,7 +104,6 @@ struct Params {
     const unsigned char *__restrict__ texels;   // all textures: RGB bytes, row-major
     const TexK *__restrict__ texs;
     float *__restrict__ out;
-    unsigned int *__restrict__ work;     // pixel work counter
     unsigned long long *__restrict__ stats;
     int nf, ns, nl;
     float bkg[3];
@@ -180,7 +179,7 @@ constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.
 #endif
 constexpr int kOrgFirst = RT_ORG_FIRST;
 constexpr double kOrgDensity = 32.0;     // objects met by a line across the scene (C3 ~3, C5 ~200)
-constexpr int kNStats = 48;              // counter slots (rt_scene_debug_counters; the device writes 0..39)
+constexpr int kNStats = 48;              // counter slots (rt_scene_debug_counters; the device writes 0..39, 44, 45)
 // RT_PROF builds: a per-wave timeline after the counters (rt_scene_debug_wavelog),
 // kWaveLogWords words per wave: launch start, prologue done, work drained (0:
 // never saw it), end (100 MHz ticks), HW_ID, XCC_ID, outer iterations, refills
@@ -191,7 +190,14 @@ constexpr int kWaveLogMax = 16384;       // waves (grid x kBlock / 64 <= 1280 x 
 constexpr int kWaveLogWords = 8;
 constexpr int kWaveLogMax = 0;
 #endif
-constexpr int kStatsAlloc = kNStats + kWaveLogWords * kWaveLogMax;
+// Pixels whose shade tree read back() of an empty medium stack (main.cpp:1028,
+// UB in the reference): stats[44] counts the events, the first kUbLogMax
+// pixels follow the counters as x << 32 | y (rt_scene_debug_ub_pixels)
+constexpr int kUbLogMax = 4096;
+constexpr int kStatsAlloc = kNStats + kUbLogMax + kWaveLogWords * kWaveLogMax;
+// The pixel work counter: a 32-bit counter in slot 45, so that the one memset
+// of the counters before a render resets it too
+constexpr int kWorkSlot = 45;
 constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS (rt_kernels.hip LW_*)
 
 // ---------------------------------------------------------------------------

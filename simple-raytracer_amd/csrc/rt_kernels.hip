@@ -1053,10 +1053,25 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
     return vadd(o, vmul(d, tt));
 }
 
+// Image coordinates of work item `pix` (defined with pixel_xy below).
+__device__ __forceinline__ void image_xy(const Params &p, unsigned pix, int &x, int &y);
+
+// back() of an empty medium stack (main.cpp:1028, undefined in the
+// reference): count it and log the pixel (stats[44] events, their pixels
+// after the counters, rt_scene_debug_ub_pixels) -- a rare branch
+__device__ __forceinline__ void ub_note(const Params &p, unsigned pix) {
+    const unsigned long long k = atomicAdd(&p.stats[44], 1ull);
+    if (k < (unsigned long long)kUbLogMax) {
+        int x, y;
+        image_xy(p, pix, x, y);
+        p.stats[kNStats + k] = ((unsigned long long)(unsigned)x << 32) | (unsigned)y;
+    }
+}
+
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
 template <int MAXF>
 __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
-                                  bool root, Counters &cnt) {
+                                  bool root, Counters &cnt, unsigned pix) {
     const int fsn = h_sn(f);
     copy_stack(f, fc, c, root);
     int n = fsn;
@@ -1071,6 +1086,7 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
             } else {
                 m.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
                 cnt.ub++;
+                ub_note(p, pix);
             }
             m.et = n > 0 ? row(p.objs, c.stack[n - 1]).eta : p.eta_bkg;
             if (n > 0) n--;
@@ -1193,7 +1209,7 @@ __device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d, i
 // set up) or until the pixel is done (returns RK_NONE with `color` set).
 // Invariant: while a node is on top, q.o is its hit point.
 template <int MAXF>
-__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color) {
+__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color, unsigned pix) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
     int top = ls.top;
     HotR h;
@@ -1255,7 +1271,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 cnt.skip++;                          // tmp_transparency stays 0
                 set_phase(h, PH_REFL);
             } else if (q.win >= 0) {
-                m = refr_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0, cnt);
+                m = refr_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0, cnt, pix);
                 set_phase(h, PH_REFR_CHILD);
                 open = true;
             } else {
@@ -1399,6 +1415,11 @@ __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, 
     y = (int)s * kStrip + (int)(r % (unsigned)sh);
 }
 
+__device__ __forceinline__ void image_xy(const Params &p, unsigned pix, int &x, int &y) {
+    pixel_xy(p, pix, x, y);
+    if (!p.pix) y = image_row(p, y);
+}
+
 // Primary ray of local pixel (x, y): p = ul + dh * x + dv * row, direction
 // (p - eye).norm() (main.cpp:720-728, that association order)
 __device__ __forceinline__ V3 primary_dir(const Params &p, int x, int y) {
@@ -1478,7 +1499,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #endif
         if (pending && !held) {
             C3 color;
-            kind = advance<MAXF>(p, ls, q, cnt, color);
+            kind = advance<MAXF>(p, ls, q, cnt, color, pix_idx);
             pending = kind != RK_NONE;
             if (!pending) {
                 // the pixel's 12 bytes in one store (global_store_dwordx3)
@@ -1519,7 +1540,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 if (n > left) {
                     unsigned g = 0;
                     const unsigned take = max(p.chunk, n - split);
-                    if (lane == leader) g = atomicAdd(p.work, take);
+                    if (lane == leader) g = atomicAdd(reinterpret_cast<unsigned *>(p.stats + kWorkSlot), take);
 #if RT_PROF
                     n_refill++;
 #endif
@@ -1678,7 +1699,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&st[8], (unsigned long long)cnt.stests);
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-        atomicMin(&st[24], t_start);                 // kernel start (first wave)
+        atomicMax(&st[24], ~t_start);                // kernel start (first wave): the counters start
+                                                     // at 0 (one memset per frame), so minima are kept
+                                                     // as maxima of the complement
         atomicMax(&st[26], t_end);                   // last wave done
     }
 #if RT_PROF
@@ -1698,7 +1721,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     {
         const unsigned w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
         if (lane == 0 && w < (unsigned)kWaveLogMax) {
-            unsigned long long *wl = st + kNStats + (size_t)w * kWaveLogWords;
+            unsigned long long *wl = st + kNStats + kUbLogMax + (size_t)w * kWaveLogWords;
             wl[0] = t_start;
             wl[1] = t_loop;
             wl[2] = t_drain;
@@ -1712,7 +1735,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     }
     if (lane == 0) {
         if (!t_drain) t_drain = t_end;
-        atomicMin(&st[25], t_drain);                 // work counter ran out
+        atomicMax(&st[25], ~t_drain);                // work counter ran out (complement, as [24])
         atomicAdd(&st[27], t_end - t_drain);         // sum of per-wave tails
         atomicAdd(&st[28], t_end - t_start);         // sum of wave lifetimes
         atomicAdd(&st[29], 1ull);                    // waves

@@ -35,7 +35,6 @@ struct RenderSlot {
     hipStream_t stream = nullptr;      // slots > 1 only (high priority: its own HW queue pool)
     hipEvent_t ev_in = nullptr;        // caller stream -> slot stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    unsigned int *work = nullptr;
     unsigned long long *stats = nullptr;
     void *d_frames = nullptr;          // ShadeRay frames of the launch
     size_t frames_cap = 0;
@@ -312,7 +311,6 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
 
 void free_slot(RenderSlot &r) {
     if (r.stream) (void)hipStreamSynchronize(r.stream);
-    if (r.work) (void)hipFree(r.work);
     if (r.stats) (void)hipFree(r.stats);
     if (r.d_frames) (void)hipFree(r.d_frames);
     if (r.ev_in) (void)hipEventDestroy(r.ev_in);
@@ -327,7 +325,6 @@ void free_slot(RenderSlot &r) {
 // queue pool per priority, so the slot's dispatches never queue behind barrier
 // packets of caller (or collective) streams that share a hardware queue.
 int init_slot(RenderSlot &r, bool own_stream) {
-    if (hipMalloc(&r.work, sizeof(unsigned)) != hipSuccess) return RT_E_NOMEM;
     if (hipMalloc(&r.stats, kStatsAlloc * sizeof(unsigned long long)) != hipSuccess) return RT_E_NOMEM;
     if (hipEventCreate(&r.ev0) != hipSuccess || hipEventCreate(&r.ev1) != hipSuccess ||
         hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming) != hipSuccess)
@@ -353,7 +350,7 @@ int set_inflight(rt_scene *s, long long n) {
         if (rc) return rc;
         // HIP binds a stream to a hardware queue at its first command: do it
         // here, not in the first frame that uses the slot
-        if (r.stream && (hipMemsetAsync(r.work, 0, sizeof(unsigned), r.stream) != hipSuccess ||
+        if (r.stream && (hipMemsetAsync(r.stats, 0, sizeof(unsigned long long), r.stream) != hipSuccess ||
                          hipStreamSynchronize(r.stream) != hipSuccess))
             return RT_E_HIP;
     }
@@ -391,12 +388,10 @@ int submit(rt_scene *s, Params &p, hipStream_t st) {
         // render (issued on whatever stream) before touching them
         return RT_E_HIP;
     }
-    p.work = slot.work;
     p.stats = slot.stats;
-    if (hipMemsetAsync(slot.work, 0, sizeof(unsigned), st) != hipSuccess) return RT_E_HIP;
+    // one reset per frame: the counters, the work counter (slot kWorkSlot) and
+    // the timeline (its minima are kept as maxima of the complement)
     if (hipMemsetAsync(slot.stats, 0, kNStats * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
-    // timeline minima start at all-ones
-    if (hipMemsetAsync(slot.stats + 24, 0xff, 2 * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
     (void)hipEventRecord(slot.ev0, st);
     int rc = launch(s, slot, p, st);
     (void)hipEventRecord(slot.ev1, st);
@@ -693,8 +688,9 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     // device time of the launch: first wave start .. last wave end (100 MHz
     // clock); the events' interval also holds any wait for a previous frame
     // still on the CUs
-    if (h[26] > h[24]) {
-        stats->kernel_ms = (double)(h[26] - h[24]) * 1e-5;
+    const unsigned long long t0 = ~h[24];          // the first wave's start (stored complemented)
+    if (h[24] != 0 && h[26] > t0) {
+        stats->kernel_ms = (double)(h[26] - t0) * 1e-5;
     } else {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, slot.ev0, slot.ev1);
@@ -711,6 +707,8 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     unsigned long long h[kNStats];
     if (hipMemcpy(h, slot.stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return RT_E_HIP;
+    // minima kept complemented on the device (one memset per frame)
+    for (int k = 24; k <= 25; k++) h[k] = h[k] ? ~h[k] : ~0ull;
     h[16] = (unsigned long long)s->last_mode;
     h[17] = (unsigned long long)s->last_blocks_per_cu;
     h[18] = (unsigned long long)s->last_grid;
@@ -727,6 +725,22 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     return RT_OK;
 }
 
+int rt_scene_debug_ub_pixels(rt_scene *s, int *xy, int n) {
+    if (!s || (n > 0 && !xy) || n < 0 || !s->last_valid) return RT_E_INVALID;
+    if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
+    const RenderSlot &slot = s->slots[(size_t)s->last_slot];
+    if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
+    unsigned long long events = 0;
+    if (hipMemcpy(&events, slot.stats + 44, sizeof events, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    const size_t k = (size_t)std::min<unsigned long long>({events, (unsigned long long)kUbLogMax,
+                                                            (unsigned long long)n});
+    std::vector<unsigned long long> v(k);
+    if (k > 0 && hipMemcpy(v.data(), slot.stats + kNStats, k * sizeof v[0], hipMemcpyDeviceToHost) != hipSuccess)
+        return RT_E_HIP;
+    for (size_t i = 0; i < k; i++) xy[2 * i] = (int)(v[i] >> 32), xy[2 * i + 1] = (int)(unsigned)v[i];
+    return (int)std::min<unsigned long long>(events, (unsigned long long)INT32_MAX);
+}
+
 int rt_scene_debug_wavelog(rt_scene *s, unsigned long long *out, int n) {
     if (kWaveLogMax == 0) return RT_E_INVALID;   // not an RT_PROF build
     if (!s || !out || n < 0 || !s->last_valid) return RT_E_INVALID;
@@ -735,7 +749,7 @@ int rt_scene_debug_wavelog(rt_scene *s, unsigned long long *out, int n) {
     if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
     const long long waves = std::min<long long>(s->last_grid * (kBlock / 64), kWaveLogMax);
     const int words = (int)std::min<long long>(n, waves * kWaveLogWords);
-    if (words > 0 && hipMemcpy(out, slot.stats + kNStats, (size_t)words * sizeof(unsigned long long),
+    if (words > 0 && hipMemcpy(out, slot.stats + kNStats + kUbLogMax, (size_t)words * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost) != hipSuccess)
         return RT_E_HIP;
     return words;

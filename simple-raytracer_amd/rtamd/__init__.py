@@ -90,7 +90,8 @@ HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
-               "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_deinterleave_rows",
+               "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_scene_debug_ub_pixels",
+               "rt_deinterleave_rows",
                "rt_strerror"]
 
 
@@ -153,6 +154,8 @@ def hip_lib() -> C.CDLL:
         L.rt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(rt_stats)]
         L.rt_scene_prepare.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int]
         L.rt_scene_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+        if hasattr(L, "rt_scene_debug_ub_pixels"):  # absent from round-1..3 libraries (A/B baselines)
+            L.rt_scene_debug_ub_pixels.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
         if hasattr(L, "rt_scene_debug_wavelog"):   # absent from round-1..3 libraries (A/B baselines)
             L.rt_scene_debug_wavelog.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
         if hasattr(L, "rt_deinterleave_rows"):
@@ -353,6 +356,18 @@ class GpuScene:
             rc = hip_lib().rt_scene_debug_counters(self._h, buf, 32)
         _check(rc, "rt_scene_debug_counters")
         return list(buf)
+
+    def debug_ub_pixels(self, cap: int = 4096):
+        """The last render's back()-of-an-empty-stack events (main.cpp:1028):
+        (events, int32 array of the first min(events, cap) events' pixels as
+        (x, y) image coordinates) -- rt_scene_debug_ub_pixels."""
+        import numpy as np
+        buf = (C.c_int * (2 * cap))()
+        n = hip_lib().rt_scene_debug_ub_pixels(self._h, buf, cap)
+        if n < 0:
+            _check(n, "rt_scene_debug_ub_pixels")
+        k = min(n, cap)
+        return n, np.array(buf[:2 * k], dtype=np.int32).reshape(k, 2)
 
     def debug_wavelog(self, max_waves: int = 16384) -> list[list[int]] | None:
         """Per-wave timeline of the last render (rt_scene_debug_wavelog; RT_PROF

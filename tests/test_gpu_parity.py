@@ -218,7 +218,7 @@ def test_c5_full_size_span_sample(tmp_path):
 def _span_sample(W: int, H: int, rows: int = 16, span: int = 64) -> np.ndarray:
     """`rows` rows spread over the image, a `span`-pixel run on each."""
     xy = []
-    for k, r in enumerate(np.linspace(0, H - 1, rows).astype(np.int64)):
+    for k, r in enumerate(np.unique(np.linspace(0, H - 1, rows).astype(np.int64))):
         x0 = (k * 1637) % (W - span)
         xy += [(x0 + i, int(r)) for i in range(span)]
     return np.array(xy, dtype=np.int32)
@@ -238,21 +238,26 @@ def _ub_pixels(o: OracleScene, W: int, H: int, xy: np.ndarray) -> list:
 def test_c5_full_size_depth8_span_sample(tmp_path):
     """BASELINE config C5 at its own setting: 16384x16384, 100 000 spheres,
     reflection + refraction at DEPTH 8 (3.8 G rays).  The whole image is
-    rendered on the GPU into HBM; 1024 pixels (64-pixel spans on 16 rows)
-    are read out and compared with the oracle at depth 8 (pinned to the
-    reference's own depth-8 floats by ref_f/C5_32x32@d8 and C5_12x12@d8).
+    rendered on the GPU into HBM; 16 384 pixels (128-pixel spans on 128
+    rows) are read out and compared with the oracle at depth 8 (pinned to
+    the reference's own depth-8 floats by ref_f/C5_32x32@d8 and C5_12x12@d8).
     The same pixels rendered alone (rt_render_pixels) give bit for bit the
-    same colours and exactly the oracle's per-type ray counts.  Pixels whose
-    shade tree reads back() of an empty medium stack (main.cpp:1028: UB in
-    the reference, defined here as eta_bkg like the oracle) are counted and
-    listed in the summary (key C5_full_d8_spans)."""
+    same colours and exactly the oracle's per-type ray counts.  Every pixel
+    of the frame whose shade tree reads back() of an empty medium stack
+    (main.cpp:1028: UB in the reference, defined here as eta_bkg like the
+    oracle) is listed by the kernel (rt_scene_debug_ub_pixels) and compared
+    with the oracle too; the list is in the summary (key C5_full_d8_spans)."""
     d = str(tmp_path)
     path = gen.write_scene(d, "C5")
     img, st, hs, gs, cam = _render_on_device(path, d, 8)
     W, H = hs.width, hs.height
     assert (W, H) == (16384, 16384) and st.primary == W * H
-    xy = _span_sample(W, H)
+    events, ubxy = gs.debug_ub_pixels()
+    assert events == st.ub_back
+    ub_px = np.unique(ubxy, axis=0).astype(np.int32) if len(ubxy) else np.zeros((0, 2), np.int32)
+    xy = _span_sample(W, H, rows=128, span=128)
     got = img[xy[:, 1].tolist(), xy[:, 0].tolist()].cpu().numpy()
+    got_ub = img[ub_px[:, 1].tolist(), ub_px[:, 0].tolist()].cpu().numpy() if len(ub_px) else None
     del img
     o = OracleScene(path, cwd=d)
     o.set_depth(8)
@@ -262,10 +267,33 @@ def test_c5_full_size_depth8_span_sample(tmp_path):
     assert np.array_equal(np.nan_to_num(alone, nan=-9), np.nan_to_num(got, nan=-9))
     assert _counts(st_px) == cnt, (_counts(st_px), cnt)
     assert cnt["refraction"] > 0 and cnt["reflection"] > 0
-    ub = _ub_pixels(o, W, H, xy) if cnt["ub_back"] else []
-    _summary["C5_full_d8_spans"] = dict(c, pixels=len(xy), gpu_total=_counts(st), sample=cnt,
-                                        ub_back_frame=int(st.ub_back), ub_back_sample_pixels=ub)
+    ub = dict(events=int(events), pixels=int(len(ub_px)))
+    if len(ub_px):
+        # the UB pixels: the oracle defines the read as eta_bkg, like the kernel
+        ref_ub, cnt_ub = o.render_pixels(W, H, ub_px)
+        ub["parity"] = assert_parity(got_ub, ref_ub, "C5 depth 8 ub_back pixels")
+        alone_ub, st_ub = gs.render_pixels(cam, W, H, ub_px)
+        assert np.array_equal(np.nan_to_num(alone_ub, nan=-9), np.nan_to_num(got_ub, nan=-9))
+        assert _counts(st_ub) == cnt_ub
+        if events <= 4096:                   # every event's pixel listed
+            assert cnt_ub["ub_back"] == events
+        ub["xy"] = ub_px.tolist()
+    _summary["C5_full_d8_spans"] = dict(c, pixels=len(xy), gpu_total=_counts(st), sample=cnt, ub_back=ub)
     gs.close()
+
+
+def test_c2_full_size_whole_image(tmp_path):
+    """BASELINE config C2 at its full 1024x1024 (100 spheres, 2 point lights,
+    no reflection / refraction): every pixel against the oracle, exact
+    per-type ray counts."""
+    d = str(tmp_path)
+    path = gen.write_scene(d, "C2")
+    img, st = rtamd.render_scene(path, cwd=d)
+    assert img.shape == (1024, 1024, 3)
+    ref, cnt = OracleScene(path, cwd=d).render()
+    c = assert_parity(img, ref, "C2 1024x1024")
+    assert _counts(st) == cnt
+    _summary["C2_full"] = dict(c, rays=cnt)
 
 
 def test_render_pixels_bit_identical():

@@ -153,6 +153,12 @@ def main() -> None:
     open(c5b, "w").write(gen.scene_text("C5", w=32, h=32))
     jobs.append(("C5_32x32@d8", c5b, work, 8))
     gen_specs["C5_32x32@d8"] = ("C5", 32, 32)
+    # ... and a 48x48 one (2304 pixels, ~33k rays; the reference runs ~10
+    # minutes on it), round 4
+    c5c = os.path.join(work, "C5_48x48.txt")
+    open(c5c, "w").write(gen.scene_text("C5", w=48, h=48))
+    jobs.append(("C5_48x48@d8", c5c, work, 8))
+    gen_specs["C5_48x48@d8"] = ("C5", 48, 48)
     for cfg in ("C3D", "C3G"):
         path = os.path.join(work, f"{cfg}_64x64.txt")
         open(path, "w").write(gen.scene_text(cfg, w=64, h=64))
