@@ -216,6 +216,9 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * (0..64, default 32: reflection / refraction searches wait until that many
  * lanes of the wave have one, unless nothing else would search) -- neither
  * changes the image,
+ * "work_parts" (-1 auto, 1 / 2 / 4 / 8: bands of the work items with a pixel counter
+ * each; auto = 8, one per XCD, when the launch has a workgroup per band --
+ * never changes the image),
  * "org_first" (-1 auto, or bits 1 shadow / 2 refraction / 4 reflection rays:
  * test the ray's origin object's BVH leaf before the search from the root;
  * auto = 6 in dense scenes, else 0 -- never changes the image),
@@ -236,7 +239,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * primary and other rays together; more launch facts: [40] origin-leaf pass
  * bits in effect (option org_first), [41] the scene's density (objects a line
  * across it meets, x1000), [42] BVH stack entries in LDS, [43] lights staged
- * in LDS (1) or read from device memory (0).  n <= 48. */
+ * in LDS (1) or read from device memory (0), [45] work bands (option work_parts).
+ * n <= 48. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 /* The last render's back() reads of an empty medium stack (main.cpp:1028,

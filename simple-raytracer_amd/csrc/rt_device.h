@@ -126,6 +126,7 @@ struct Params {
     unsigned chunk;                      // work items a wave takes from the counter at a time (0: its idle lanes' count)
     unsigned refill_min;                 // refill only when at least this many lanes are idle (or all are)
     unsigned gate_x;                     // hold reflection/refraction searches until this many lanes have one
+    unsigned work_shift;                 // 2^work_shift work item bands with a counter each (3: one per XCD)
     void *__restrict__ frames;           // grid x kBlock x MAXF cold ShadeRay frames
     int *__restrict__ ovf;               // grid x kBlock x ovf_stride spilled BVH stack entries
     const int *__restrict__ pix;         // pixel list (x, y pairs; rt_render_pixels) or null: work item k
@@ -179,7 +180,7 @@ constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.
 #endif
 constexpr int kOrgFirst = RT_ORG_FIRST;
 constexpr double kOrgDensity = 32.0;     // objects met by a line across the scene (C3 ~3, C5 ~200)
-constexpr int kNStats = 48;              // counter slots (rt_scene_debug_counters; the device writes 0..39, 44, 45)
+constexpr int kNStats = 48;              // counter slots (rt_scene_debug_counters; the device writes 0..39, 44)
 // RT_PROF builds: a per-wave timeline after the counters (rt_scene_debug_wavelog),
 // kWaveLogWords words per wave: launch start, prologue done, work drained (0:
 // never saw it), end (100 MHz ticks), HW_ID, XCC_ID, outer iterations, refills
@@ -190,14 +191,21 @@ constexpr int kWaveLogMax = 16384;       // waves (grid x kBlock / 64 <= 1280 x 
 constexpr int kWaveLogWords = 8;
 constexpr int kWaveLogMax = 0;
 #endif
+// Pixel work counters after the counters: one per band of the work items
+// (Params::work_parts bands, one per XCD: workgroup b runs on XCD b mod 8),
+// each a 32-bit counter in a 128-B line of its own; the one memset before a
+// render (kStatsReset slots) resets them with the counters.
+constexpr int kWorkSlots = kNStats;      // band b's counter: u64 slot kWorkSlots + kWorkStride * b
+constexpr int kWorkStride = 16;
+constexpr int kWorkPartsMax = 8;
+constexpr int kStatsReset = kWorkSlots + kWorkStride * kWorkPartsMax;
 // Pixels whose shade tree read back() of an empty medium stack (main.cpp:1028,
 // UB in the reference): stats[44] counts the events, the first kUbLogMax
-// pixels follow the counters as x << 32 | y (rt_scene_debug_ub_pixels)
+// pixels follow the work counters as x << 32 | y (rt_scene_debug_ub_pixels)
+constexpr int kUbLogOff = kStatsReset;
 constexpr int kUbLogMax = 4096;
-constexpr int kStatsAlloc = kNStats + kUbLogMax + kWaveLogWords * kWaveLogMax;
-// The pixel work counter: a 32-bit counter in slot 45, so that the one memset
-// of the counters before a render resets it too
-constexpr int kWorkSlot = 45;
+constexpr int kWaveLogOff = kUbLogOff + kUbLogMax;
+constexpr int kStatsAlloc = kWaveLogOff + kWaveLogWords * kWaveLogMax;
 constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS (rt_kernels.hip LW_*)
 
 // ---------------------------------------------------------------------------

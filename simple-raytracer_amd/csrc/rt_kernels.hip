@@ -1064,7 +1064,7 @@ __device__ __forceinline__ void ub_note(const Params &p, unsigned pix) {
     if (k < (unsigned long long)kUbLogMax) {
         int x, y;
         image_xy(p, pix, x, y);
-        p.stats[kNStats + k] = ((unsigned long long)(unsigned)x << 32) | (unsigned)y;
+        p.stats[kUbLogOff + k] = ((unsigned long long)(unsigned)x << 32) | (unsigned)y;
     }
 }
 
@@ -1466,6 +1466,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     int held_kind = RK_NONE;
     bool drained = false;      // wave saw the work counter run out
     unsigned chunk_pos = 0, chunk_end = 0;   // the wave's tile: its unused work items [pos, end)
+    // the wave's band of the work items (uniform, one register): bits 0-3 the
+    // band (its XCD's first, then the next ones), 4-7 the bands not yet
+    // exhausted, bit 8: no batch taken yet (the static first batch)
+    unsigned wband = (blockIdx.x & ((1u << p.work_shift) - 1u)) | (1u << (p.work_shift + 4)) | (p.chunk == 0 ? 256u : 0u);
     unsigned pix_idx = 0;      // the lane's work item (its pixel's (x, y) is recomputed for the store)
 #if RT_PROF >= 2
     cnt.t_fetch = cnt.t_trip = 0;
@@ -1524,6 +1528,15 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         // few new primaries.  Idle lanes sit out the steps until then
         // (C3 +10 %, C4 +30 %, C5 +50 % against refilling every idle lane at
         // once; see refill_for).
+        //
+        // Work items come in p.work_parts bands (8: one per XCD, workgroup b
+        // runs on XCD b mod 8) with a counter each; a wave starts on its
+        // XCD's band and moves to the next band when its own runs out.  Its
+        // first batch is assigned statically (wave k of the band: items
+        // [64 k, 64 k + 64) of it; the band's counter counts from there):
+        // 5120 waves asking one counter at once, and again whenever their
+        // batches end together, is what held short frames back (C2: 160 us
+        // per trace step, profiles/r04/timeline_C2.json).
         if (!drained) {
             unsigned long long idle = __ballot(!busy);
             if (idle && ((unsigned)__popcll(idle) >= p.refill_min || idle == ~0ull)) {
@@ -1536,18 +1549,40 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 // current chunk, the others the start of the next one.
                 const unsigned left = chunk_end - chunk_pos;
                 const unsigned base = chunk_pos, split = min(n, left);
+                const unsigned sh = p.work_shift, P = 1u << sh, band = wband & 15u;
+                // the items taken below are of this band: [band_lo, cur_end)
+                const unsigned band_lo = (unsigned)(((unsigned long long)band * p.total) >> sh);
+                const unsigned cur_end = (unsigned)(((unsigned long long)(band + 1) * p.total) >> sh);
                 unsigned nbase = 0;
                 if (n > left) {
-                    unsigned g = 0;
                     const unsigned take = max(p.chunk, n - split);
-                    if (lane == leader) g = atomicAdd(reinterpret_cast<unsigned *>(p.stats + kWorkSlot), take);
+                    // work items the band's waves take statically, before its counter
+                    const unsigned nstatic = ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
+                    unsigned g;
+                    if (wband & 256u) {
+                        // (the wave's index, uniform: readfirstlane keeps g in an SGPR)
+                        g = ((blockIdx.x >> sh) * (unsigned)(kBlock / 64) +
+                             (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64))) * 64u;
+                    } else {
+                        g = 0;
+                        if (lane == leader)
+                            g = nstatic + atomicAdd(reinterpret_cast<unsigned *>(p.stats + kWorkSlots + kWorkStride * band),
+                                                    take);
+                        g = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
 #if RT_PROF
-                    n_refill++;
+                        n_refill++;
 #endif
-                    nbase = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
+                    }
+                    nbase = band_lo + g;
                     chunk_pos = nbase + (n - split);
                     chunk_end = nbase + take;
-                    if (nbase >= p.total) drained = true;
+                    wband &= ~256u;
+                    if (nbase >= cur_end) {              // this band is done: the next one
+                        chunk_pos = chunk_end = 0;
+                        wband -= 16u;
+                        if ((wband >> 4) == 0) drained = true;
+                        wband = (wband & ~15u) | (band + 1 == P ? 0u : band + 1);
+                    }
                 } else {
                     chunk_pos += n;
                 }
@@ -1558,7 +1593,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     // idle lanes below this one (v_mbcnt: no per-lane mask kept in registers)
                     unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
                     unsigned idx = rank < split ? base + rank : nbase + (rank - split);
-                    if (idx < p.total) {
+                    if (idx < cur_end) {
                         int px, py;
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
@@ -1721,7 +1756,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     {
         const unsigned w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
         if (lane == 0 && w < (unsigned)kWaveLogMax) {
-            unsigned long long *wl = st + kNStats + kUbLogMax + (size_t)w * kWaveLogWords;
+            unsigned long long *wl = st + kWaveLogOff + (size_t)w * kWaveLogWords;
             wl[0] = t_start;
             wl[1] = t_loop;
             wl[2] = t_drain;

@@ -63,6 +63,7 @@ struct rt_scene {
     long long opt_grid = 0;            // blocks (0 = occupancy-derived)
     long long opt_chunk = -1;          // refill chunk (-1: default, chunk_for)
     long long opt_refill_min = -1;     // idle lanes before a refill (-1: by the scene, refill_for)
+    long long opt_work_parts = -1;     // work item bands with a counter each (-1: one per XCD when the launch allows)
     bool secondary = false;            // some material reflects (ks > 0) or refracts (opacity < 1, eta > 0)
     long long opt_reserve = 0;         // occupancy-derived grid: block slots left free for other kernels
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
@@ -86,7 +87,7 @@ struct rt_scene {
     bool bvh_ok = false;
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
-    long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0;
+    long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0, last_work_parts = 0;
     long long bvh_nodes = 0;
     bool last_valid = false;
 };
@@ -164,6 +165,13 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     if (grid < 1) grid = 1;
     pl.chunk = chunk_for(s);
     pl.refill_min = refill_for(s, pl);
+    // work bands: one per XCD (workgroup b runs on XCD b mod 8: its L2), unless
+    // the launch is too small to give each band a workgroup (option work_parts)
+    const unsigned parts = s->opt_work_parts > 0 ? (unsigned)s->opt_work_parts
+                           : (grid >= kWorkPartsMax && p.total >= (unsigned)(kWorkPartsMax * kBlock))
+                               ? (unsigned)kWorkPartsMax
+                               : 1u;
+    pl.work_shift = parts >= 8 ? 3 : parts >= 4 ? 2 : parts >= 2 ? 1 : 0;
     const size_t cold_bytes = (size_t)grid * kBlock * maxf * cold_frame_bytes(maxf);
     size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
     if (slot.frames_cap < fbytes) {
@@ -187,6 +195,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     s->last_org_first = pl.org_first;
     s->last_stack_cap = pl.stack_cap;
     s->last_lights_in_lds = pl.lights_in_lds;
+    s->last_work_parts = 1 << pl.work_shift;
     if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
     return render_launch(maxf, mode, pl, (unsigned)grid, shm, st);
 }
@@ -389,9 +398,9 @@ int submit(rt_scene *s, Params &p, hipStream_t st) {
         return RT_E_HIP;
     }
     p.stats = slot.stats;
-    // one reset per frame: the counters, the work counter (slot kWorkSlot) and
+    // one reset per frame: the counters, the work counters (kWorkSlots) and
     // the timeline (its minima are kept as maxima of the complement)
-    if (hipMemsetAsync(slot.stats, 0, kNStats * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
+    if (hipMemsetAsync(slot.stats, 0, kStatsReset * sizeof(unsigned long long), st) != hipSuccess) return RT_E_HIP;
     (void)hipEventRecord(slot.ev0, st);
     int rc = launch(s, slot, p, st);
     (void)hipEventRecord(slot.ev1, st);
@@ -543,6 +552,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
     else if (k == "refill_min") {
         if (value < 1 || value > 64) return RT_E_INVALID;
         s->opt_refill_min = value;
+    }
+    else if (k == "work_parts") {
+        if (value != -1 && value != 1 && value != 2 && value != 4 && value != 8) return RT_E_INVALID;
+        s->opt_work_parts = value;
     }
     else if (k == "chunk") {
         if (value < 0 || value > 4096) return RT_E_INVALID;
@@ -721,6 +734,7 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[41] = (unsigned long long)(s->crossings * 1000.0);
     h[42] = (unsigned long long)s->last_stack_cap;
     h[43] = (unsigned long long)s->last_lights_in_lds;
+    h[45] = (unsigned long long)s->last_work_parts;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }
@@ -735,7 +749,7 @@ int rt_scene_debug_ub_pixels(rt_scene *s, int *xy, int n) {
     const size_t k = (size_t)std::min<unsigned long long>({events, (unsigned long long)kUbLogMax,
                                                             (unsigned long long)n});
     std::vector<unsigned long long> v(k);
-    if (k > 0 && hipMemcpy(v.data(), slot.stats + kNStats, k * sizeof v[0], hipMemcpyDeviceToHost) != hipSuccess)
+    if (k > 0 && hipMemcpy(v.data(), slot.stats + kUbLogOff, k * sizeof v[0], hipMemcpyDeviceToHost) != hipSuccess)
         return RT_E_HIP;
     for (size_t i = 0; i < k; i++) xy[2 * i] = (int)(v[i] >> 32), xy[2 * i + 1] = (int)(unsigned)v[i];
     return (int)std::min<unsigned long long>(events, (unsigned long long)INT32_MAX);
@@ -749,7 +763,7 @@ int rt_scene_debug_wavelog(rt_scene *s, unsigned long long *out, int n) {
     if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
     const long long waves = std::min<long long>(s->last_grid * (kBlock / 64), kWaveLogMax);
     const int words = (int)std::min<long long>(n, waves * kWaveLogWords);
-    if (words > 0 && hipMemcpy(out, slot.stats + kNStats + kUbLogMax, (size_t)words * sizeof(unsigned long long),
+    if (words > 0 && hipMemcpy(out, slot.stats + kWaveLogOff, (size_t)words * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost) != hipSuccess)
         return RT_E_HIP;
     return words;
