@@ -95,14 +95,24 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned r) {
 //  shadow  : every intersection of every object != self with tmin < t (and
 //            t < tmax unless unbounded) multiplies mask by (1 - opacity)
 //            (main.cpp:898-912, :930-949)
+// The shadow mask (main.cpp:788) is grey: it starts at {1,1,1} and every
+// occluder multiplies all three channels by the same factor (1 - opacity),
+// so it is kept as one float.  A shadow query multiplies its own light's
+// factors from 1 (q.mask); the cumulative mask of the node's earlier lights
+// rides in q.back (as float bits: back is a SKIP_TRANS field, unused by shadow
+// queries) and the light step multiplies the two (advance, PH_LIGHT): the
+// same product as the reference's running one, reassociated (all factors in
+// [0, 1]: relaxation 3 of DESIGN.md §5), and the same bits whichever lane
+// traced the ray (RT_SHADOW_HELP).
 struct Query {
     V3 o, d;
     float tmin, tmax;
     int self, back, win;
     bool closest, unb, skipchk, skipped;
     bool bf;                              // BVH mode: this query needs the brute-force scan
-    C3 mask;
+    float mask;                           // shadow: product of this light's factors so far
 };
+__device__ __forceinline__ float prior_mask(const Query &q) { return __int_as_float(q.back); }
 
 constexpr float kInf = __builtin_huge_valf();
 
@@ -121,9 +131,9 @@ __device__ __forceinline__ void offer(Query &q, float t, int obj, const float *_
             }
         } else {
             float f = cst(ofac)[obj];
-            q.mask = cmulf(q.mask, f);
+            q.mask = clamp01(f * q.mask);
             // an opaque occluder zeroes the mask for good: any-hit termination
-            if ((q.mask.r == 0.0f) & (q.mask.g == 0.0f) & (q.mask.b == 0.0f)) q.tmin = kInf;
+            if (q.mask == 0.0f) q.tmin = kInf;
         }
     }
 }
@@ -388,8 +398,8 @@ __device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, 
                 if (fac == 0.0f && p.shadow_early_out) {
                     opaque = true;
                 } else if (!PRE) {
-                    if (s0) q.mask = cmulf(q.mask, fac);
-                    if (s1) q.mask = cmulf(q.mask, fac);
+                    if (s0) q.mask = clamp01(fac * q.mask);
+                    if (s1) q.mask = clamp01(fac * q.mask);
                 }
             }
         }
@@ -708,7 +718,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     } else if (q.skipchk) {
         q.skipped = opaque;
     } else if (opaque) {
-        q.mask = {0.0f, 0.0f, 0.0f};
+        q.mask = 0.0f;
     }
 }
 
@@ -753,7 +763,7 @@ __device__ __forceinline__ int h_sn(const HotR &h) { return (int)((h.meta >> 4) 
 // meta bit 31 (RT_SHADOW_HELP): the next light's shadow ray was traced by an
 // idle lane in the same step, its factors' product waits in this lane's
 // stack entries 1..3
-constexpr unsigned kMetaTwo = 1u << 31;
+[[maybe_unused]] constexpr unsigned kMetaTwo = 1u << 31;
 __device__ __forceinline__ int h_light(const HotR &h) { return (int)((h.meta >> 9) & 0x3fffffu); }
 __device__ __forceinline__ unsigned mk_meta(int phase, int state, int sn, int light) {
     return (unsigned)phase | ((unsigned)state << 3) | ((unsigned)sn << 4) | ((unsigned)light << 9);
@@ -1214,6 +1224,7 @@ __device__ __forceinline__ void shadow_query(Query &q, const Params &p, int ligh
     q.skipchk = false;
     q.skipped = false;
     q.win = -1;
+    q.mask = 1.0f;                   // this light's factors, from 1 (the prior mask is the caller's, q.back)
 }
 
 __device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d, int org) {
@@ -1281,7 +1292,11 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
                 C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
                 C3 lc = {lw1.x, lw1.y, lw1.z};
-                h.acc = cadd(h.acc, cmulc(cmulc(lc, q.mask), cadd(dc, sc)));
+                // the cumulative mask after this light: the earlier lights'
+                // times this light's factors (one product, reassociated)
+                const float mcum = clamp01(q.mask * prior_mask(q));
+                h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), cadd(dc, sc)));
+                q.back = __float_as_int(mcum);
                 light++;
 #if RT_SHADOW_HELP
                 if (!two || pass) break;
@@ -1289,8 +1304,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
                 // ray: this light's times the product of the next ray's
                 // factors, which the helper lane multiplied from 1 (all in
                 // [0, 1]: a reassociation, relaxation 3 of DESIGN.md §5)
-                const float *mb = lane_stack();
-                q.mask = cmulc(q.mask, C3{mb[1 * kBlock], mb[2 * kBlock], mb[3 * kBlock]});
+                q.mask = lane_stack()[1 * kBlock];
             }
             h.meta = (h.meta & ~kMetaTwo) + ((two ? 2u : 1u) << 9);   // next light
 #else
@@ -1352,7 +1366,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         ls.top = top;
         if (p.nl > 0) {                              // shadow ray for light 0 (main.cpp:885-928)
             shadow_query(q, p, 0, q.win);
-            q.mask = C3{1.0f, 1.0f, 1.0f};           // the node's first light (main.cpp:788)
+            q.back = __float_as_int(1.0f);           // the node's first light: mask {1,1,1} (main.cpp:788)
             return RK_SHADOW;
         }
         lds_load(h);                                 // no lights: straight to the light loop's end
@@ -1672,8 +1686,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         // factor is in [0, 1] when none is NaN (shadow_early_out), and
         // clamp01(0 * f) = 0.  It is still a TraceRay call of the reference
         // (counted above); its result is known without searching.
-        const bool known = pending && !q.closest && p.shadow_early_out && (q.mask.r == 0.0f) &
-                           (q.mask.g == 0.0f) & (q.mask.b == 0.0f);
+        const bool known = pending && !q.closest && p.shadow_early_out && prior_mask(q) == 0.0f;
         // Reflection / refraction searches (closest hit, the longest after
         // the primaries) are held back until at least p.gate_x lanes of the
         // wave have one, unless nothing else would search in this step: like
@@ -1719,9 +1732,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 if (helper) {
                     q.o = V3{ox, oy, oz};
                     shadow_query(q, p, olt + 1, oself);
-                    q.mask = C3{1.0f, 1.0f, 1.0f};
-                    q.win = -2;                      // marks the helper until its product is handed back
-                    q.back = owner;
+                    q.back = __float_as_int(1.0f);   // (its own prior mask: searched in full)
+                    q.win = -2 - owner;              // marks the helper and its owner until the product is handed back
                     // its light for the cone pass (h_light_lds): an idle lane's LDS state is free
                     lane_lds()[LW_META * kBlock] = __uint_as_float(mk_meta(PH_LIGHT, 0, 0, olt + 1));
                 }
@@ -1774,7 +1786,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             // unless the faces already made the mask 0 for good
             if (p.dir_bf == 2) {
                 const bool pt = search && !q.closest && q.unb && !q.bf &&
-                                !(p.shadow_early_out && (q.mask.r == 0.0f) & (q.mask.g == 0.0f) & (q.mask.b == 0.0f));
+                                !(p.shadow_early_out && q.mask == 0.0f);
                 if (__ballot(pt) && pt) {
                     const DirK &dk = p.dirk[h_light_lds()];
                     const int root = dk.root;
@@ -1806,11 +1818,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #if RT_SHADOW_HELP
             // helpers hand their products to the owners' stack entries 1..3
             // (free: every search of the step has ended), and are idle again
-            if (q.win == -2) {
-                float *ob = reinterpret_cast<float *>(lds) + (threadIdx.x & ~63u) + q.back;
-                ob[1 * kBlock] = q.mask.r;
-                ob[2 * kBlock] = q.mask.g;
-                ob[3 * kBlock] = q.mask.b;
+            if (q.win <= -2) {
+                float *ob = reinterpret_cast<float *>(lds) + (threadIdx.x & ~63u) + (-2 - q.win);
+                ob[1 * kBlock] = q.mask;
                 q.win = -1;
                 q.tmin = kInf;
             }
