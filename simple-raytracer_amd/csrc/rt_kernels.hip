@@ -1618,7 +1618,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 if (n > left) {
                     const unsigned take = max(p.chunk, n - split);
                     // work items the band's waves take statically, before its counter
-                    const unsigned nstatic = ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
+                    // (none when they take chunks: option chunk)
+                    const unsigned nstatic = p.chunk ? 0u : ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
                     unsigned g;
                     if (wband & 256u) {
                         // (the wave's index, uniform: readfirstlane keeps g in an SGPR)

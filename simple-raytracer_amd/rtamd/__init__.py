@@ -297,7 +297,14 @@ class GpuScene:
         (host) or an int device pointer; returns (out, rt_stats)."""
         st = rt_stats()
         if out is None:
-            out = np.empty((y1 - y0, W, 3), dtype=np.float32)
+            # into a device buffer filled with NaN first: a pixel the kernel
+            # never wrote shows up (a host buffer goes through the library's
+            # staging buffer, which may still hold an earlier render)
+            import torch
+            dev = torch.full((y1 - y0, W, 3), float("nan"), dtype=torch.float32, device=f"cuda:{self.device}")
+            _check(hip_lib().rt_render_rows(self._h, C.byref(cam), W, H, y0, y1, C.c_void_p(dev.data_ptr()),
+                                            C.byref(st)), "rt_render_rows")
+            return dev.cpu().numpy(), st
         ptr = out if isinstance(out, int) else out.ctypes.data
         _check(hip_lib().rt_render_rows(self._h, C.byref(cam), W, H, y0, y1, C.c_void_p(ptr),
                                         C.byref(st)), "rt_render_rows")
