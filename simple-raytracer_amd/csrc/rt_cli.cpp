@@ -175,7 +175,9 @@ int main(int argc, char *argv[]) {
     rt_camera cam;
     rth_camera(hs, W, H, &cam);
 
-    int ndev = rt_device_count();
+    t = Clock::now();
+    int ndev = rt_device_count();                // the HIP runtime starts here
+    const double ph_hip_init = ms_since(t);
     if (ndev < 1) {
         std::cerr << "rt: no HIP device" << std::endl;
         return 2;
@@ -192,7 +194,9 @@ int main(int argc, char *argv[]) {
         std::cerr << "rt: --gather must be rccl or host" << std::endl;
         return 2;
     }
+    t = Clock::now();
     std::vector<float> img((size_t)W * H * 3);
+    const double ph_alloc = ms_since(t);
     std::vector<rt_stats> st(gpus);
     std::vector<int> rcs(gpus, 0);
     std::vector<std::thread> pool;
@@ -306,11 +310,12 @@ int main(int argc, char *argv[]) {
         if (f) {
             fprintf(f,
                     "{\"scene\": \"%s\", \"imsize\": [%d, %d], \"depth\": %d, \"gpus\": %d, \"gather\": \"%s\", "
-                    "\"rays\": %llu, \"phases_ms\": {\"parse\": %.3f, \"scene_upload\": %.3f, \"bvh_build\": %.3f, "
+                    "\"rays\": %llu, \"phases_ms\": {\"parse\": %.3f, \"hip_init\": %.3f, \"host_image_alloc\": %.3f, "
+                    "\"scene_upload\": %.3f, \"bvh_build\": %.3f, "
                     "\"bvh_build_host\": %.3f, \"render\": %.3f, \"kernel\": %.3f, \"d2h\": %.3f, "
                     "\"quantise_ppm_write\": %.3f}, \"total_ms\": %.3f, \"ppm_bytes\": %lld, "
                     "\"Mrays_per_s_end_to_end\": %.3f, \"Mrays_per_s_kernel\": %.3f}\n",
-                    argv[1], W, H, eff_depth, gpus, gather.c_str(), rays, ph_parse, ph_create, ph_bvh, bvh_host, ph_render,
+                    argv[1], W, H, eff_depth, gpus, gather.c_str(), rays, ph_parse, ph_hip_init, ph_alloc, ph_create, ph_bvh, bvh_host, ph_render,
                     kms, ph_d2h, ph_write, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
             if (f != stderr) fclose(f);
         }

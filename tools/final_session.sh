@@ -1,9 +1,12 @@
 #!/bin/bash
 # End-of-round evidence on one GPU box (all outputs under gpurun_out/final/):
 # smoke, the GPU test suite, one bench line per config, a rocprofv3 kernel
-# trace of the default bench at one frame in flight and at two, and the PMC
-# passes whose FETCH_SIZE / WRITE_SIZE give profiles/pmc_traffic.json.  Every
-# GPU step has its own time limit; the script stops at the first failure.
+# trace of the default bench at one frame in flight and at two, the PMC
+# passes whose FETCH_SIZE / WRITE_SIZE give profiles/pmc_traffic.json
+# (tools/pmc_traffic.py; recorded with the library's sha), the projected
+# N-GPU balance (tools/rank_balance.py), the one-shot CLI phases
+# (tools/e2e.py) and a wave timeline of C2.  Every GPU step has its own time
+# limit; the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
@@ -11,8 +14,10 @@ export TMPDIR=/tmp
 O=$R/gpurun_out/final
 mkdir -p $O
 step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+PART=${PART:-all}
+if [ "$PART" = all ] || [ "$PART" = a ]; then
 step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
-step tests bash -c "timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=\$?; tail -2 $O/pytest_gpu.log; exit \$rc"
+step tests bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=\$?; tail -2 $O/pytest_gpu.log; exit \$rc"
 step bench_C3 bash -c "timeout -k 10 600 python bench.py > $O/C3_bench.json 2> $O/C3_bench.err"
 for c in C2 C3D C3G; do
   step bench_$c bash -c "timeout -k 10 600 python bench.py --config $c --cpu-baseline off --steps 100 > $O/${c}_bench.json 2> $O/${c}_bench.err"
@@ -20,10 +25,16 @@ done
 for c in C4 C5; do
   step bench_$c bash -c "timeout -k 10 600 python bench.py --config $c --cpu-baseline off --steps 8 --warmup 2 > $O/${c}_bench.json 2> $O/${c}_bench.err"
 done
+step e2e bash -c "timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 > $O/e2e.txt 2>&1"
+for c in C3 C4 C5; do
+  step bal_$c bash -c "timeout -k 10 600 python -u tools/rank_balance.py $c --ns 1,2,4,8 > $O/${c}_row_balance.txt 2>&1"
+done
+fi
+if [ "$PART" = all ] || [ "$PART" = b ]; then
 cd /tmp
 step prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --cpu-baseline off --steps 5 --inflight 1
 step prof2 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_inflight2 -o run --output-format csv -- python3 $R/bench.py --cpu-baseline off --steps 20 --inflight 2
-for c in C4 C5; do
+for c in C2 C4 C5; do
   step prof_$c timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run --output-format csv -- python3 $R/bench.py --config $c --cpu-baseline off --steps 3 --warmup 1 --inflight 1
 done
 i=0
@@ -37,16 +48,19 @@ WRITE_SIZE
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU
 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_THREAD_CYCLES_VALU TA_BUSY_avr
 TCC_HIT_sum TCC_MISS_sum
+TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum
 PASSES
 cd $R
 RENDERS=2 python3 tools/pmc_summary.py $O/pmc > $O/C3_pmc.json
 cd /tmp
 for c in C4 C5; do
-  for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+  for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum"; do
     n=$(echo $ctr | cut -d' ' -f1)
     step pmc_${c}_$n timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $O/pmc_$c/p_$n -o run --output-format csv -- python3 $R/bench.py --config $c --cpu-baseline off --steps 1 --warmup 0 --inflight 1
   done
 done
 cd $R
 for c in C4 C5; do RENDERS=2 python3 tools/pmc_summary.py $O/pmc_$c > $O/${c}_pmc.json; done
+step timeline bash -c "RTAMD_LIB_DIR=$R/simple-raytracer_amd/lib_prof timeout -k 10 200 python -u tools/timeline.py C2 > $O/tl_C2.txt 2>&1"
+fi
 echo done
