@@ -1530,7 +1530,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     // the wave's band of the work items (uniform, one register): bits 0-3 the
     // band (its XCD's first, then the next ones), 4-7 the bands not yet
     // exhausted, bit 8: no batch taken yet (the static first batch)
-    unsigned wband = (blockIdx.x & ((1u << p.work_shift) - 1u)) | (1u << (p.work_shift + 4)) | (p.chunk == 0 ? 256u : 0u);
+#ifndef RT_STATIC_FIRST
+#define RT_STATIC_FIRST 1                // 0: the first batch from the counter too (A/B)
+#endif
+    unsigned wband = (blockIdx.x & ((1u << p.work_shift) - 1u)) | (1u << (p.work_shift + 4)) |
+                     (p.chunk == 0 && RT_STATIC_FIRST ? 256u : 0u);
     unsigned pix_idx = 0;      // the lane's work item (its pixel's (x, y) is recomputed for the store)
 #if RT_PROF >= 2
     cnt.t_fetch = cnt.t_trip = 0;
@@ -1619,7 +1623,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     const unsigned take = max(p.chunk, n - split);
                     // work items the band's waves take statically, before its counter
                     // (none when they take chunks: option chunk)
-                    const unsigned nstatic = p.chunk ? 0u : ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
+                    const unsigned nstatic =
+                        p.chunk || !RT_STATIC_FIRST ? 0u : ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
                     unsigned g;
                     if (wband & 256u) {
                         // (the wave's index, uniform: readfirstlane keeps g in an SGPR)
