@@ -195,11 +195,12 @@ constexpr int kWaveLogWords = 8;
 constexpr int kWaveLogMax = 0;
 #endif
 // Pixel work counters after the counters: one per band of the work items
-// (Params::work_parts bands, one per XCD: workgroup b runs on XCD b mod 8),
-// each a 32-bit counter in a 128-B line of its own; the one memset before a
-// render (kStatsReset slots) resets them with the counters.
+// (2^Params::work_shift bands, one per XCD: workgroup b runs on XCD b mod 8),
+// each a 32-bit counter 4 KB from the next (device-scope atomics are done
+// memory-side: counters on one channel would queue behind each other); the
+// one memset before a render (kStatsReset slots) resets them with the counters.
 constexpr int kWorkSlots = kNStats;      // band b's counter: u64 slot kWorkSlots + kWorkStride * b
-constexpr int kWorkStride = 16;
+constexpr int kWorkStride = 512;
 constexpr int kWorkPartsMax = 8;
 constexpr int kStatsReset = kWorkSlots + kWorkStride * kWorkPartsMax;
 // Pixels whose shade tree read back() of an empty medium stack (main.cpp:1028,

@@ -1614,40 +1614,52 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 // current chunk, the others the start of the next one.
                 const unsigned left = chunk_end - chunk_pos;
                 const unsigned base = chunk_pos, split = min(n, left);
-                const unsigned sh = p.work_shift, P = 1u << sh, band = wband & 15u;
-                // the items taken below are of this band: [band_lo, cur_end)
-                const unsigned band_lo = (unsigned)(((unsigned long long)band * p.total) >> sh);
-                const unsigned cur_end = (unsigned)(((unsigned long long)(band + 1) * p.total) >> sh);
-                unsigned nbase = 0;
+                const unsigned sh = p.work_shift, P = 1u << sh;
+                // the current chunk's items are of the current band: [.., old_end)
+                const unsigned old_end = (unsigned)(((unsigned long long)((wband & 15u) + 1) * p.total) >> sh);
+                unsigned nbase = 0, new_end = 0;
                 if (n > left) {
                     const unsigned take = max(p.chunk, n - split);
-                    // work items the band's waves take statically, before its counter
-                    // (none when they take chunks: option chunk)
-                    const unsigned nstatic =
-                        p.chunk || !RT_STATIC_FIRST ? 0u : ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
-                    unsigned g;
-                    if (wband & 256u) {
-                        // (the wave's index, uniform: readfirstlane keeps g in an SGPR)
-                        g = ((blockIdx.x >> sh) * (unsigned)(kBlock / 64) +
-                             (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64))) * 64u;
-                    } else {
-                        g = 0;
-                        if (lane == leader)
-                            g = nstatic + atomicAdd(reinterpret_cast<unsigned *>(p.stats + kWorkSlots + kWorkStride * band),
-                                                    take);
-                        g = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
+                    // a band that has run out: the next one, at once (a wave
+                    // leaves only when every band has run out)
+                    for (;;) {
+                        const unsigned band = wband & 15u;
+                        const unsigned band_lo = (unsigned)(((unsigned long long)band * p.total) >> sh);
+                        new_end = (unsigned)(((unsigned long long)(band + 1) * p.total) >> sh);
+                        // work items the band's waves take statically, before its counter
+                        // (none when they take chunks: option chunk)
+                        const unsigned nstatic =
+                            p.chunk || !RT_STATIC_FIRST ? 0u : ((gridDim.x - band + P - 1) >> sh) * (unsigned)kBlock;
+                        unsigned g;
+                        if (wband & 256u) {
+                            // (the wave's index, uniform: readfirstlane keeps g in an SGPR)
+                            g = ((blockIdx.x >> sh) * (unsigned)(kBlock / 64) +
+                                 (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64))) * 64u;
+                        } else {
+                            g = 0;
+                            if (lane == leader)
+                                g = nstatic + atomicAdd(reinterpret_cast<unsigned *>(p.stats + kWorkSlots +
+                                                                                     kWorkStride * band),
+                                                        take);
+                            g = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
 #if RT_PROF
-                        n_refill++;
+                            n_refill++;
 #endif
-                    }
-                    nbase = band_lo + g;
-                    chunk_pos = nbase + (n - split);
-                    chunk_end = nbase + take;
-                    wband &= ~256u;
-                    if (nbase >= cur_end) {              // this band is done: the next one
-                        chunk_pos = chunk_end = 0;
+                        }
+                        wband &= ~256u;
+                        nbase = band_lo + g;
+                        if (nbase < new_end) {
+                            chunk_pos = nbase + (n - split);
+                            chunk_end = nbase + take;
+                            break;
+                        }
+                        chunk_pos = chunk_end = 0;      // this band is done
                         wband -= 16u;
-                        if ((wband >> 4) == 0) drained = true;
+                        if ((wband >> 4) == 0) {
+                            drained = true;
+                            new_end = 0;
+                            break;
+                        }
                         wband = (wband & ~15u) | (band + 1 == P ? 0u : band + 1);
                     }
                 } else {
@@ -1660,7 +1672,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     // idle lanes below this one (v_mbcnt: no per-lane mask kept in registers)
                     unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
                     unsigned idx = rank < split ? base + rank : nbase + (rank - split);
-                    if (idx < cur_end) {
+                    if (idx < (rank < split ? old_end : new_end)) {
                         int px, py;
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
