@@ -143,9 +143,6 @@ enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 #ifndef RT_PRIO
 #define RT_PRIO 1                        // 1: shading steps at wave priority 2 (render_kernel)
 #endif
-#ifndef RT_SHADOW_HELP
-#define RT_SHADOW_HELP 0                 // 1: idle lanes trace the next light's shadow ray of a node (render_kernel)
-#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif

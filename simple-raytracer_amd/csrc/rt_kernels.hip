@@ -70,22 +70,6 @@ __device__ __forceinline__ const T &row(const T *base, int i) {
     return base[i];
 }
 
-// position of the (r+1)-th set bit of m (r < popcount(m)): a binary search
-// over the halves by popcount
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned r) {
-    int pos = 0;
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) {
-        const unsigned c = (unsigned)__popcll(m & ((1ull << w) - 1ull));
-        if (r >= c) {
-            r -= c;
-            m >>= w;
-            pos += w;
-        }
-    }
-    return pos;
-}
-
 // ---------------------------------------------------------------------------
 // One lane's ray query (a TraceRay call + the consumer loop that follows it)
 // ---------------------------------------------------------------------------
@@ -102,8 +86,9 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, unsigned r) {
 // rides in q.back (as float bits: back is a SKIP_TRANS field, unused by shadow
 // queries) and the light step multiplies the two (advance, PH_LIGHT): the
 // same product as the reference's running one, reassociated (all factors in
-// [0, 1]: relaxation 3 of DESIGN.md §5), and the same bits whichever lane
-// traced the ray (RT_SHADOW_HELP).
+// [0, 1]: relaxation 3 of DESIGN.md §5).  (Round 4 measured idle lanes
+// tracing a node's next light in the same step on this representation: C3
+// -3 %)
 struct Query {
     V3 o, d;
     float tmin, tmax;
@@ -760,11 +745,7 @@ struct HotR {                        // register form of the top node's state
 __device__ __forceinline__ int h_phase(const HotR &h) { return (int)(h.meta & 7u); }
 __device__ __forceinline__ int h_state(const HotR &h) { return (int)((h.meta >> 3) & 1u); }
 __device__ __forceinline__ int h_sn(const HotR &h) { return (int)((h.meta >> 4) & 31u); }
-// meta bit 31 (RT_SHADOW_HELP): the next light's shadow ray was traced by an
-// idle lane in the same step, its factors' product waits in this lane's
-// stack entries 1..3
-[[maybe_unused]] constexpr unsigned kMetaTwo = 1u << 31;
-__device__ __forceinline__ int h_light(const HotR &h) { return (int)((h.meta >> 9) & 0x3fffffu); }
+__device__ __forceinline__ int h_light(const HotR &h) { return (int)(h.meta >> 9); }
 __device__ __forceinline__ unsigned mk_meta(int phase, int state, int sn, int light) {
     return (unsigned)phase | ((unsigned)state << 3) | ((unsigned)sn << 4) | ((unsigned)light << 9);
 }
@@ -809,11 +790,7 @@ __device__ __forceinline__ LightW light_words(const Params &p, int i) {
 }
 
 __device__ __forceinline__ float *lane_lds() { return reinterpret_cast<float *>(rt_lds) + threadIdx.x; }
-__device__ __forceinline__ int h_light_lds() {
-    return (int)((__float_as_uint(lane_lds()[LW_META * kBlock]) >> 9) & 0x3fffffu);
-}
-// this lane's BVH stack entries in LDS (entry e at [e * kBlock]), after the state
-__device__ __forceinline__ float *lane_stack() { return reinterpret_cast<float *>(rt_lds) + kLdsHot * kBlock + threadIdx.x; }
+__device__ __forceinline__ int h_light_lds() { return (int)(__float_as_uint(lane_lds()[LW_META * kBlock]) >> 9); }
 __device__ __forceinline__ void lds_load(HotR &h) {
     const float *l = lane_lds();
     h.N = {l[(LW_N + 0) * kBlock], l[(LW_N + 1) * kBlock], l[(LW_N + 2) * kBlock]};
@@ -1266,62 +1243,40 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters 
         lds_load(h);
         const int phase = h_phase(h);
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
-            int light = h_light(h);
+            const int light = h_light(h);
             const ObjK &ob = row(p.objs, h.obj);
-#if RT_SHADOW_HELP
-            const bool two = (h.meta & kMetaTwo) != 0;
-#pragma unroll 1
-            for (int pass = 0;; pass++) {
-#endif
-                // the light's words in one batch (LightK: xyz w | col | L)
-                const LightW lw = light_words(p, light);
-                const f4v lw0 = lw.w0, lw1 = lw.w1, lw2 = lw.w2;
-                // L as light_vectors computed it for the shadow ray just traced:
-                // that ray's direction for a point light, the constant -L for a
-                // directional one (q.d is not modified by a trace)
-                V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
-#if RT_SHADOW_HELP
-                // the second light's ray went to another lane: its L as
-                // light_vectors computes it (main.cpp:921)
-                if (pass && lw0.w != 0.0f) L = vnorm(vsub(V3{lw0.x, lw0.y, lw0.z}, q.o));
-#endif
-                // H only feeds the specular power: rsqrt instead of 3 IEEE
-                // divisions (<= 2 ulp; vnorm(0) = NaN either way)
-                V3 hv = vadd(L, h.I);
-                V3 H = vmul(hv, __builtin_amdgcn_rsqf(vdot(hv, hv)));
-                C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
-                C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
-                C3 lc = {lw1.x, lw1.y, lw1.z};
-                // the cumulative mask after this light: the earlier lights'
-                // times this light's factors (one product, reassociated)
-                const float mcum = clamp01(q.mask * prior_mask(q));
-                h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), cadd(dc, sc)));
-                q.back = __float_as_int(mcum);
-                light++;
-#if RT_SHADOW_HELP
-                if (!two || pass) break;
-                // the cumulative mask (main.cpp:788) after the next light's
-                // ray: this light's times the product of the next ray's
-                // factors, which the helper lane multiplied from 1 (all in
-                // [0, 1]: a reassociation, relaxation 3 of DESIGN.md §5)
-                q.mask = lane_stack()[1 * kBlock];
-            }
-            h.meta = (h.meta & ~kMetaTwo) + ((two ? 2u : 1u) << 9);   // next light
-#else
+            // the light's words in one batch (LightK: xyz w | col | L)
+            const LightW lw = light_words(p, light);
+            const f4v lw0 = lw.w0, lw1 = lw.w1, lw2 = lw.w2;
+            // L as light_vectors computed it for the shadow ray just traced:
+            // that ray's direction for a point light, the constant -L for a
+            // directional one (q.d is not modified by a trace)
+            V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
+            // H only feeds the specular power: rsqrt instead of 3 IEEE
+            // divisions (<= 2 ulp; vnorm(0) = NaN either way)
+            V3 hv = vadd(L, h.I);
+            V3 H = vmul(hv, __builtin_amdgcn_rsqf(vdot(hv, hv)));
+            C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
+            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
+            C3 lc = {lw1.x, lw1.y, lw1.z};
+            // the cumulative mask after this light: the earlier lights'
+            // times this light's factors (one product, reassociated)
+            const float mcum = clamp01(q.mask * prior_mask(q));
+            h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), cadd(dc, sc)));
+            q.back = __float_as_int(mcum);
             h.meta += 1u << 9;                       // next light
-#endif
             // stored at once, in the block that computed it: kept in registers
             // across the other phases' code of the shading step, the colour
             // was spilled to scratch and reloaded -- a reload whose vmcnt wait
             // also waited for the frame stores of lanes that opened a child
             lds_store_light(h);
-            if (light < p.nl) {
+            if (light + 1 < p.nl) {
                 // next light's shadow ray from the same point: origin, self
                 // and cumulative mask are already in q (main.cpp:885-928)
                 // (opaque index: reusing this light's address for the next
                 // one kept a 64-bit pointer live -- and spilled -- across the
                 // shading code)
-                int next = light;
+                int next = light + 1;
                 asm volatile("" : "+v"(next));
                 shadow_query(q, p, next, h.obj);
                 ls.top = top;
@@ -1721,51 +1676,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             held = sec && others && nsec < p.gate_x;
             held_kind = k;
         }
-        bool search = pending && !known && !held;
-#if RT_SHADOW_HELP
-        // Second shadow rays on idle lanes.  A lane tracing the shadow ray of
-        // light l of its node (l + 1 < nl) offers the next light's ray; the
-        // wave's idle lanes (no pixel: waiting for a refill batch, or the
-        // work is done) take the offers rank by rank and trace them in this
-        // same step, from 1 instead of the cumulative mask.  The owner
-        // shades both lights in its next step (advance, PH_LIGHT): a node's
-        // light loop takes one step per two lights where a helper is free.
-        bool helper = false;
-        if (MODE == MODE_BVH && p.nl > 1) {
-            const int lt = h_light_lds();            // the light of this lane's shadow ray (if any)
-            const bool offer = search && kind == RK_SHADOW && lt + 1 < p.nl;
-            const unsigned long long of = __ballot(offer), id = __ballot(!pending);
-            const unsigned m = min((unsigned)__popcll(of), (unsigned)__popcll(id));
-            if (m) {
-                const unsigned orank = __builtin_amdgcn_mbcnt_hi((unsigned)(of >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)of, 0u));
-                if (offer && orank < m) {
-                    float *mw = lane_lds() + LW_META * kBlock;
-                    *mw = __uint_as_float(__float_as_uint(*mw) | kMetaTwo);
-                }
-                const unsigned hrank = __builtin_amdgcn_mbcnt_hi((unsigned)(id >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)id, 0u));
-                helper = !pending && hrank < m;
-                const int owner = nth_set_bit(of, helper ? hrank : 0u);
-                const float ox = __shfl(q.o.x, owner), oy = __shfl(q.o.y, owner), oz = __shfl(q.o.z, owner);
-                const int oself = __shfl(q.self, owner), olt = __shfl(lt, owner);
-                if (helper) {
-                    q.o = V3{ox, oy, oz};
-                    shadow_query(q, p, olt + 1, oself);
-                    q.back = __float_as_int(1.0f);   // (its own prior mask: searched in full)
-                    q.win = -2 - owner;              // marks the helper and its owner until the product is handed back
-                    // its light for the cone pass (h_light_lds): an idle lane's LDS state is free
-                    lane_lds()[LW_META * kBlock] = __uint_as_float(mk_meta(PH_LIGHT, 0, 0, olt + 1));
-                }
-            }
-        }
-        search = search || helper;
-#endif
+        const bool search = pending && !known && !held;
 
         w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
-#if RT_SHADOW_HELP
-        w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW || helper));
-#else
         w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
-#endif
         w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
         w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
         w_known += (unsigned)__popcll(__ballot(known));
@@ -1832,16 +1746,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             if (nb) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
 #if RT_PROF
             pc_bf += __builtin_amdgcn_s_memtime() - c2;
-#endif
-#if RT_SHADOW_HELP
-            // helpers hand their products to the owners' stack entries 1..3
-            // (free: every search of the step has ended), and are idle again
-            if (q.win <= -2) {
-                float *ob = reinterpret_cast<float *>(lds) + (threadIdx.x & ~63u) + (-2 - q.win);
-                ob[1 * kBlock] = q.mask;
-                q.win = -1;
-                q.tmin = kInf;
-            }
 #endif
         } else {
             scan<SRC_LDS>(q, p, lds_f, lds_s, search, cnt.ftests, cnt.stests);
