@@ -1504,7 +1504,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
     unsigned long long pc_mixed = 0;     // trace steps with primary and secondary/shadow searches together
     unsigned long long t_drain = 0;
-    unsigned long long n_refill = 0;
+    unsigned long long n_refill = 0, pc_refill = 0;
     const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_first = 0;      // end of the first trace step (its code fetched cold)
 #endif
@@ -1535,7 +1535,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 if (!p.pix)
 #endif
                     pixel_xy(p, pix_idx, px, py);
+#ifndef RT_AB_NOSTORE                // (A/B probe only: no framebuffer store)
                 *reinterpret_cast<f3v *>(p.out + ((size_t)py * p.W + px) * 3) = f3v{color.r, color.g, color.b};
+#else
+                if (color.r == -1.0f) p.out[0] = (float)px + (float)py;
+#endif
                 busy = false;
             }
         }
@@ -1592,6 +1596,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                                  (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64))) * 64u;
                         } else {
                             g = 0;
+#if RT_PROF
+                            const unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
                             if (lane == leader)
                                 g = nstatic + atomicAdd(reinterpret_cast<unsigned *>(p.stats + kWorkSlots +
                                                                                      kWorkStride * band),
@@ -1599,6 +1606,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                             g = (unsigned)__builtin_amdgcn_readlane((int)g, leader);   // uniform: an SGPR
 #if RT_PROF
                             n_refill++;
+                            pc_refill += __builtin_amdgcn_s_memtime() - ta;   // the counter's round trip
 #endif
                         }
                         wband &= ~256u;
@@ -1781,6 +1789,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[13], pc_lanes);
         atomicAdd(&st[14], pc_wtrips);
         atomicAdd(&st[39], pc_mixed);
+        atomicAdd(&st[46], pc_refill);               // cycles waiting for the work counter
+        atomicAdd(&st[47], n_refill);
     }
     atomicAdd(&st[15], (unsigned long long)cnt.trips);
     atomicAdd(&st[36], (unsigned long long)cnt.trips_kind[0]);

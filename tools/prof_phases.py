@@ -61,6 +61,9 @@ def main():
     res = {
         "config": cfg, "objects": kw, "rows": rows, "options": opts, "kernel_ms": st.kernel_ms,
         "cycles_split": {"shade_refill": shade / tot, "trace": trace / tot, "bf_scan": bf / tot} if tot else None,
+        # of shade_refill: waiting for the work counter's atomic (RT_PROF, round 4)
+        "work_counter_wait_frac": c[46] / tot if tot else None,
+        "work_counter_wait_cycles_per_refill": c[46] / c[47] if c[47] else None,
         "outer_iterations": iters,
         "trace_lane_occupancy": lanes / (64 * iters) if iters else None,
         "traversal_simd_eff": ltrips / (64 * wtrips) if wtrips else None,
