@@ -222,6 +222,10 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
  * "org_first" (-1 auto, or bits 1 shadow / 2 refraction / 4 reflection rays:
  * test the ray's origin object's BVH leaf before the search from the root;
  * auto = 6 in dense scenes, else 0 -- never changes the image),
+ * "hot_copies" (0, or a power of 2 up to 64: copies of the main BVH's top
+ * 64 nodes and their leaves, each wave starting its searches in one of them --
+ * spreads the reads every search makes of the root over L2 channels; never
+ * changes the image),
  * "fail_bvh_upload" (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
@@ -239,7 +243,8 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * primary and other rays together; more launch facts: [40] origin-leaf pass
  * bits in effect (option org_first), [41] the scene's density (objects a line
  * across it meets, x1000), [42] BVH stack entries in LDS, [43] lights staged
- * in LDS (1) or read from device memory (0), [45] work bands (option work_parts).
+ * in LDS (1) or read from device memory (0), [44] copies of the BVH's top in
+ * effect (option hot_copies), [45] work bands (option work_parts).
  * n <= 48. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 

@@ -115,6 +115,8 @@ struct Params {
     unsigned int total;                  // W * rows, or the pixel list's length
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
+    int hot_base, hot_stride;            // copies of the main tree's top (rt_accel.h kHotNodes): the root
+    unsigned hot_mask;                   // wave w starts at bvh + hot_base + (w & hot_mask) * hot_stride bytes
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
     int dir_bf;                          // directional lights in a scene with spheres: 0 none,
                                          // 1 brute-force scan, 2 faces by the BVH + shadow-region trees

@@ -643,10 +643,16 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
     }
     if (point)
         node = root;
-    else if (!ended)
-        visit_q(sld4b(p.bvh, 0), near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff), neg_x),
-                near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff + 24), neg_y),
-                near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff + 48), neg_z), sld4b(p.bvh, rtbvh::kNodeLinkOff));
+    else if (!ended) {
+        // this wave's copy of the top of the tree (Params::hot_mask; the
+        // index counts the waves of one XCD: blockIdx.x / 8)
+        const int hw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x >> 3) * (kBlock / 64) + threadIdx.x / 64));
+        const int r0 = p.hot_base + (int)((unsigned)hw & p.hot_mask) * p.hot_stride;
+        visit_q(sld4b(p.bvh, r0), near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff), neg_x),
+                near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff + 24), neg_y),
+                near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff + 48), neg_z),
+                sld4b(p.bvh, r0 + rtbvh::kNodeLinkOff));
+    }
     for (;;) {
         while (node >= 0) {
 #if RT_PROF >= 2

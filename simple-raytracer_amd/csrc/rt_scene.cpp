@@ -74,6 +74,7 @@ struct rt_scene {
     long long opt_fail_bvh_upload = 0; // test hook: the next BVH uploads fail (RT_E_NOMEM)
     AccelInput in;                     // host arrays + BVH sources (rt_accel.h)
     long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
+    long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
     float4 *d_leafrec = nullptr;
@@ -88,6 +89,7 @@ struct rt_scene {
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
     long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0, last_work_parts = 0;
+    long long last_hot_copies = 0;
     long long bvh_nodes = 0;
     bool last_valid = false;
 };
@@ -209,6 +211,7 @@ int build_bvh(rt_scene *s, double D) {
     o.collapse = (int)s->opt_bvh_collapse;
     o.node_milli = (int)s->opt_bvh_node;
     o.threads = (int)s->opt_bvh_threads;
+    o.hot_copies = (int)s->opt_hot_copies;
     AccelTree T;
     build_accel(s->in, D, o, T);
     bool ok = T.ok;
@@ -228,18 +231,25 @@ int build_bvh(rt_scene *s, double D) {
         ok = false;
     }
     if (ok) {
-        const size_t node_bytes = QQ.size() * sizeof(QQ[0]);
+        const size_t main_bytes = QQ.size() * sizeof(QQ[0]);
+        const size_t node_bytes = T.hot_copies > 1 ? T.hot_base + (size_t)T.hot_copies * T.hot_stride : main_bytes;
         const size_t dir_bytes = std::max<size_t>(1, dirk.size()) * sizeof(DirK);
         if (hipMalloc(&nb, node_bytes) != hipSuccess ||
             hipMalloc(&nr, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess ||
             hipMalloc(&nd, dir_bytes) != hipSuccess || hipMalloc(&nl, objleaf.size() * sizeof(int32_t)) != hipSuccess)
             rc = RT_E_NOMEM;
-        else if (hipMemcpy(nb, QQ.data(), node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        else if (hipMemcpy(nb, QQ.data(), main_bytes, hipMemcpyHostToDevice) != hipSuccess ||
                  hipMemcpy(nr, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess ||
                  (!dirk.empty() && hipMemcpy(nd, dirk.data(), dirk.size() * sizeof(DirK), hipMemcpyHostToDevice) !=
                                        hipSuccess) ||
                  hipMemcpy(nl, objleaf.data(), objleaf.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
             rc = RT_E_HIP;
+        for (int c = 0; !rc && c < (T.hot_copies > 1 ? T.hot_copies : 0); c++) {
+            const size_t per = (size_t)T.hot_per_copy * sizeof(QQ[0]);
+            if (hipMemcpy(reinterpret_cast<char *>(nb) + T.hot_base + (size_t)c * T.hot_stride,
+                          T.hot_nodes.data() + (size_t)c * T.hot_per_copy, per, hipMemcpyHostToDevice) != hipSuccess)
+                rc = RT_E_HIP;
+        }
         if (rc) {
             if (nb) (void)hipFree(nb);
             if (nr) (void)hipFree(nr);
@@ -267,6 +277,11 @@ int build_bvh(rt_scene *s, double D) {
     s->base.leafrec = nr;
     s->base.dirk = nd;
     s->base.dir_bf = T.dir_mode;
+    const bool hot = ok && rc == RT_OK && T.hot_copies > 1;
+    s->base.hot_base = hot ? (int)T.hot_base : 0;
+    s->base.hot_stride = hot ? (int)T.hot_stride : 0;
+    s->base.hot_mask = hot ? (unsigned)(T.hot_copies - 1) : 0u;
+    s->last_hot_copies = hot ? T.hot_copies : 0;
     s->bvh_ok = ok && rc == RT_OK;
     s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
     s->bvh_depth = s->bvh_ok ? T.depth : 0;
@@ -572,6 +587,11 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         else s->opt_bvh_node = std::max(0LL, value);
         s->bvh_D = -1.0;               // rebuild on the next render
     }
+    else if (k == "hot_copies") {
+        if (value < 0 || value > 64 || (value & (value - 1))) return RT_E_INVALID;
+        s->opt_hot_copies = value;
+        s->bvh_D = -1.0;
+    }
     else return RT_E_INVALID;
     return RT_OK;
 }
@@ -735,6 +755,7 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[42] = (unsigned long long)s->last_stack_cap;
     h[43] = (unsigned long long)s->last_lights_in_lds;
     h[45] = (unsigned long long)s->last_work_parts;
+    h[44] = (unsigned long long)s->last_hot_copies;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }

@@ -63,7 +63,8 @@ def bvh_bench():
 @pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
 def test_bvh_build_threads_identical(bvh_bench, tmp_path, cfg):
     """The host build on 4 threads gives the serial build's trees bit for bit,
-    and both are the pinned trees of the seeded scene (no GPU)."""
+    and both are the pinned trees of the seeded scene (no GPU); a build with
+    hot copies of the tree's top holds the same tree from every copy's root."""
     import json
     from rtamd import scenes as gen
     path = gen.write_scene(str(tmp_path), cfg)
@@ -72,3 +73,6 @@ def test_bvh_build_threads_identical(bvh_bench, tmp_path, cfg):
     j = json.loads(r.stdout)
     assert j["identical"] and j["ok"] == 1, j
     assert j["hash"] == BENCH_TREE_HASH[cfg], j
+    # 16 hot copies of the top (option hot_copies): each copy's walk reads
+    # the main tree's bounds and leaf records, the main arrays unchanged
+    assert j["hot_ok"] and j["hot_copies"] == 16 and j["hot_per_copy"] == min(64, j["main_nodes"]), j

@@ -726,6 +726,38 @@ def test_refill_options_bit_identical():
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
 
+def test_work_bands_and_hot_copies_bit_identical():
+    """Option work_parts (bands of the work items with a pixel counter each,
+    auto = one per XCD) and option hot_copies (copies of the BVH's top 64
+    nodes and their leaves; each wave starts its searches in one) change
+    which lane renders which pixel and where a search reads the tree's top,
+    never a pixel: the image and ray counts equal the default render's bit
+    for bit, which equals the oracle's.  C2 has fewer nodes than one copy
+    holds (the whole tree is copied), C5 at depth 8 has 37 864."""
+    variants = [{"work_parts": w} for w in (1, 2, 4, 8)]
+    variants += [{"hot_copies": k} for k in (0, 2, 16, 64)] + [{"hot_copies": 16, "work_parts": 1, "chunk": 100}]
+    for name, depth in (("C2_128x128.txt", None), ("C3_64x64.txt", None), ("C5_8x8.txt", 8)):
+        ref, st = rtamd.render_scene(name, cwd=SCENES, depth=depth)
+        o = OracleScene(name, cwd=SCENES)
+        if depth:
+            o.set_depth(depth)
+        oi, o_cnt = o.render()
+        assert_parity(ref, oi, f"{name} default")
+        assert _counts(st) == o_cnt
+        for opts in variants:
+            img, st2 = rtamd.render_scene(name, cwd=SCENES, depth=depth, options=opts)
+            assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, opts)
+            assert _counts(st2) == _counts(st), (name, opts)
+    hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
+    gs = rtamd.GpuScene(hs)
+    gs.set_option("hot_copies", 16)
+    gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
+    assert gs.debug_counters()[44] == 16
+    for bad in ({"hot_copies": 3}, {"hot_copies": 128}, {"work_parts": 3}):
+        with pytest.raises(rtamd.RTError):
+            rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
+
+
 @pytest.mark.parametrize("opts", [{"gate_x": 64, "refill_min": 64}, {"gate_x": 64, "refill_min": 1}, {"gate_x": 0, "refill_min": 64}])
 def test_extreme_batching_deep_scene(opts):
     """The batching options at their extremes on a depth-8 C5 miniature (long
