@@ -202,6 +202,15 @@ constexpr int kWorkSlots = kNStats;      // band b's counter: u64 slot kWorkSlot
 constexpr int kWorkStride = 512;
 constexpr int kWorkPartsMax = 8;
 constexpr int kStatsReset = kWorkSlots + kWorkStride * kWorkPartsMax;
+// The exit-time counters of every wave ([0..8], [24], [26], [32..34]) go to
+// kStatCopies copies of the counter array, copy c in the free words of band
+// (c mod 8)'s counter block, 512 B or 1.5 KB past the counter: thousands of
+// waves ending within microseconds of each other, each adding to the same
+// few words, queued behind each other in one memory channel.  The host folds
+// the copies (sum; maximum for [24] and [26]).
+constexpr int kStatCopies = 16;
+constexpr int stat_copy_off(int c) { return kWorkSlots + kWorkStride * (c & 7) + 64 + (c >> 3) * 128; }
+static_assert(64 + 128 + kNStats <= kWorkStride, "stat copies fit a band's counter block");
 // Pixels whose shade tree read back() of an empty medium stack (main.cpp:1028,
 // UB in the reference): stats[44] counts the events, the first kUbLogMax
 // pixels follow the work counters as x << 32 | y (rt_scene_debug_ub_pixels)

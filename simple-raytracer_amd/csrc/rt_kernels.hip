@@ -223,6 +223,7 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 struct Counters {
     unsigned skip, ub;
     unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
+    unsigned spills;                            // BVH stack blocks moved to device memory
 #if RT_PROF
     unsigned trips;                             // traversal loop iterations of this lane
     unsigned trips_kind[3];                     // ... of primary / shadow / refraction + reflection queries
@@ -532,7 +533,11 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         for (int i = kSpill + 1; i < sp; i++) stk[(i - kSpill) * kBlock] = stk[i * kBlock];
         sp -= kSpill;
         stk[0] = kRefill + nb + 1;
-        atomicAdd(&p.stats[34], 1ull);
+#ifndef RT_AB_SPILL_ATOMIC
+        cnt.spills++;
+#else                                    // (A/B: the count by an atomic per spill, no register)
+        atomicAdd(&p.stats[stat_copy_off((int)(blockIdx.x & (kStatCopies - 1))) + 34], 1ull);
+#endif
     };
     // pop the top entry, whose value n the caller has already read (stk[sp - 1])
     auto pop_value = [&](int n) -> int {
@@ -1473,7 +1478,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     LaneState<MAXF> ls;
     ls.top = -1;
     ls.frames = p.frames;
-    Counters cnt = {0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;
     int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
@@ -1766,25 +1771,30 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         }
     }
     unsigned long long *st = p.stats;
+    // this workgroup's copy of the exit counters (rt_device.h kStatCopies)
+    unsigned long long *sc = st + stat_copy_off((int)(blockIdx.x & (kStatCopies - 1)));
+#ifndef RT_AB_NOSTATS                        // (A/B probe only: no exit counters but the clock)
     if (lane == 0) {
-        atomicAdd(&st[0], w_prim);
-        atomicAdd(&st[1], w_shadow);
-        atomicAdd(&st[2], w_refr);
-        atomicAdd(&st[3], w_refl);
-        atomicAdd(&st[32], (unsigned long long)w_known);
-        atomicAdd(&st[33], (unsigned long long)w_bf);
+        atomicAdd(&sc[0], w_prim);
+        atomicAdd(&sc[1], w_shadow);
+        atomicAdd(&sc[2], w_refr);
+        atomicAdd(&sc[3], w_refl);
+        atomicAdd(&sc[32], (unsigned long long)w_known);
+        atomicAdd(&sc[33], (unsigned long long)w_bf);
     }
-    atomicAdd(&st[4], (unsigned long long)cnt.skip);
-    atomicAdd(&st[5], (unsigned long long)cnt.ub);
-    atomicAdd(&st[6], (unsigned long long)cnt.boxes);
-    atomicAdd(&st[7], (unsigned long long)cnt.ftests);
-    atomicAdd(&st[8], (unsigned long long)cnt.stests);
+    atomicAdd(&sc[4], (unsigned long long)cnt.skip);
+    atomicAdd(&sc[5], (unsigned long long)cnt.ub);
+    atomicAdd(&sc[6], (unsigned long long)cnt.boxes);
+    atomicAdd(&sc[7], (unsigned long long)cnt.ftests);
+    atomicAdd(&sc[8], (unsigned long long)cnt.stests);
+    atomicAdd(&sc[34], (unsigned long long)cnt.spills);
+#endif
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-        atomicMax(&st[24], ~t_start);                // kernel start (first wave): the counters start
+        atomicMax(&sc[24], ~t_start);                // kernel start (first wave): the counters start
                                                      // at 0 (one memset per frame), so minima are kept
                                                      // as maxima of the complement
-        atomicMax(&st[26], t_end);                   // last wave done
+        atomicMax(&sc[26], t_end);                   // last wave done
     }
 #if RT_PROF
     if (lane == 0) {

@@ -514,6 +514,8 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.chunk = 0;                       // launch_one: chunk_for, refill_for
     p.refill_min = 1;
     p.gate_x = kGateX;
+    p.hot_base = p.hot_stride = 0;     // set with the BVH (build_bvh)
+    p.hot_mask = 0;
     // The origin-leaf pass for reflection and refraction rays pays in dense
     // scenes (C5: +2.3 %) and costs sparse ones (C3: -1.1 %;
     // profiles/r03/ab_origin_leaf.txt); the density is AccelInput::crossings
@@ -697,6 +699,23 @@ int rt_render_rows_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0
     return rt_render_row_blocks_async(s, cam, W, H, y0, y1 - y0, y1 - y0, y1 - y0, out_rgb, hip_stream);
 }
 
+// The last render's counters with the exit counters' copies folded in
+// (rt_device.h kStatCopies).
+static hipError_t read_counters(const RenderSlot &slot, unsigned long long h[kNStats]) {
+    std::vector<unsigned long long> all(kStatsReset);
+    hipError_t e = hipMemcpy(all.data(), slot.stats, all.size() * sizeof(all[0]), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    std::memcpy(h, all.data(), kNStats * sizeof(h[0]));
+    static const int kAdd[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 32, 33, 34};
+    for (int c = 0; c < kStatCopies; c++) {
+        const unsigned long long *sc = all.data() + stat_copy_off(c);
+        for (int k : kAdd) h[k] += sc[k];
+        h[24] = std::max(h[24], sc[24]);
+        h[26] = std::max(h[26], sc[26]);
+    }
+    return hipSuccess;
+}
+
 int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     if (!s || !stats) return RT_E_INVALID;
     if (!s->last_valid) return RT_E_INVALID;
@@ -704,7 +723,7 @@ int rt_scene_last_stats(rt_scene *s, rt_stats *stats) {
     const RenderSlot &slot = s->slots[(size_t)s->last_slot];
     if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
     unsigned long long h[kNStats];
-    if (hipMemcpy(h, slot.stats, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_E_HIP;
+    if (read_counters(slot, h) != hipSuccess) return RT_E_HIP;
     stats->primary = h[0];
     stats->shadow = h[1];
     stats->refraction = h[2];
@@ -738,8 +757,7 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     const RenderSlot &slot = s->slots[(size_t)s->last_slot];
     if (hipEventSynchronize(slot.ev1) != hipSuccess) return RT_E_HIP;
     unsigned long long h[kNStats];
-    if (hipMemcpy(h, slot.stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-        return RT_E_HIP;
+    if (read_counters(slot, h) != hipSuccess) return RT_E_HIP;
     // minima kept complemented on the device (one memset per frame)
     for (int k = 24; k <= 25; k++) h[k] = h[k] ? ~h[k] : ~0ull;
     h[16] = (unsigned long long)s->last_mode;
