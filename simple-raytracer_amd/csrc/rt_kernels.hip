@@ -223,7 +223,6 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 struct Counters {
     unsigned skip, ub;
     unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
-    unsigned spills;                            // BVH stack blocks moved to device memory
 #if RT_PROF
     unsigned trips;                             // traversal loop iterations of this lane
     unsigned trips_kind[3];                     // ... of primary / shadow / refraction + reflection queries
@@ -533,11 +532,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bo
         for (int i = kSpill + 1; i < sp; i++) stk[(i - kSpill) * kBlock] = stk[i * kBlock];
         sp -= kSpill;
         stk[0] = kRefill + nb + 1;
-#ifndef RT_AB_SPILL_ATOMIC
-        cnt.spills++;
-#else                                    // (A/B: the count by an atomic per spill, no register)
+        // counted in the workgroup's copy of the exit counters: a per-lane
+        // counter held in a register costs more (C3 -0.5 %, ab_stat_copies.txt)
         atomicAdd(&p.stats[stat_copy_off((int)(blockIdx.x & (kStatCopies - 1))) + 34], 1ull);
-#endif
     };
     // pop the top entry, whose value n the caller has already read (stk[sp - 1])
     auto pop_value = [&](int n) -> int {
@@ -1478,7 +1475,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     LaneState<MAXF> ls;
     ls.top = -1;
     ls.frames = p.frames;
-    Counters cnt = {0, 0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;
     int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
@@ -1647,6 +1644,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
                     unsigned idx = rank < split ? base + rank : nbase + (rank - split);
                     if (idx < (rank < split ? old_end : new_end)) {
+                        // option order: the k-th full segment handed out is seg_order[k]
+                        if (p.seg_order && idx / (unsigned)kSeg < p.seg_full)
+                            idx = p.seg_order[idx / (unsigned)kSeg] * (unsigned)kSeg + idx % (unsigned)kSeg;
                         int px, py;
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
@@ -1787,7 +1787,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     atomicAdd(&sc[6], (unsigned long long)cnt.boxes);
     atomicAdd(&sc[7], (unsigned long long)cnt.ftests);
     atomicAdd(&sc[8], (unsigned long long)cnt.stests);
-    atomicAdd(&sc[34], (unsigned long long)cnt.spills);
 #endif
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
@@ -1854,6 +1853,98 @@ __global__ void deinterleave_kernel(const float *__restrict__ gathered, int worl
     float *dst = image + (size_t)y * n;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------
+// Segment order (option order): the costliest work first
+// ---------------------------------------------------------------------------
+// A frame lasts until its last pixel is done, and pixels differ by two orders
+// of magnitude: one whose primary ray meets glass opens a tree of up to
+// 2^depth refraction and reflection nodes, ~100 traces one after the other in
+// its lane, while a diffuse pixel takes 3.  Handed out in image order, the
+// costly pixels of the last work items set the frame's tail (C3: the last
+// ~1.1 ms of 13 with fewer and fewer waves alive; at N = 8 half of a rank's
+// frame, profiles/r04/timeline_*.json).  Longest first: the full segments of
+// kSeg work items go out by a cost class sampled at one item each -- its
+// primary ray's nearest object: 2 refracting (opacity < 1, eta > 0, the test
+// of the shading code), 1 reflecting (ks > 0), 0 anything else or a miss --
+// class 2 first, in image order within a class.  Which lane renders which
+// pixel when changes; no pixel does.
+__global__ void __launch_bounds__(kBlock) seg_class_kernel(Params p, unsigned nseg, unsigned char *__restrict__ cls) {
+    int *stk = reinterpret_cast<int *>(rt_lds) + threadIdx.x;   // the traversal stack, entries kBlock apart
+    stk[0] = rtbvh::kEmpty;
+    Counters cnt = {0, 0, 0, 0, 0};
+    for (unsigned k = blockIdx.x * kBlock + threadIdx.x; k < nseg; k += gridDim.x * kBlock) {
+        int px, py;
+        pixel_xy(p, k * (unsigned)kSeg + (unsigned)kSegSample, px, py);
+        Query q;
+        q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
+        q.d = primary_dir(p, px, py);
+        q.tmin = 0.0f;
+        q.tmax = kFltMax;
+        q.unb = false;
+        q.self = -1;
+        q.back = -1;
+        q.win = -1;
+        q.closest = true;
+        q.skipchk = q.skipped = q.bf = false;
+        q.mask = 1.0f;
+        bvh_trace<false>(q, p, stk, cnt);
+        unsigned char c = 0;
+        if (q.win >= 0) {
+            const ObjK &o = p.objs[q.win];
+            c = ((double)o.opacity < 1.0 && o.eta > 0) ? 2 : (double)o.ks > 0.0 ? 1 : 0;
+        }
+        cls[k] = c;
+    }
+}
+
+// Stable counting sort of the segments by class (2, 1, 0) in one workgroup:
+// thread t counts its contiguous run of segments, a scan over the threads
+// gives each run its offsets, and each thread writes its run in order.
+__global__ void __launch_bounds__(kOrderThreads) seg_order_kernel(const unsigned char *__restrict__ cls, unsigned nseg,
+                                                                 unsigned *__restrict__ order) {
+    __shared__ unsigned sc[3][kOrderThreads];
+    const unsigned t = threadIdx.x;
+    const unsigned per = (nseg + kOrderThreads - 1) / kOrderThreads;
+    const unsigned b = min(nseg, t * per), e = min(nseg, b + per);
+    unsigned n0 = 0, n1 = 0, n2 = 0;
+    for (unsigned k = b; k < e; k++) {
+        const unsigned c = cls[k];
+        n0 += c == 0;
+        n1 += c == 1;
+        n2 += c == 2;
+    }
+    sc[0][t] = n0;
+    sc[1][t] = n1;
+    sc[2][t] = n2;
+    __syncthreads();
+    // inclusive scan over the threads (Hillis-Steele), each class
+    for (unsigned d = 1; d < kOrderThreads; d <<= 1) {
+        unsigned a0 = 0, a1 = 0, a2 = 0;
+        if (t >= d) a0 = sc[0][t - d], a1 = sc[1][t - d], a2 = sc[2][t - d];
+        __syncthreads();
+        sc[0][t] += a0;
+        sc[1][t] += a1;
+        sc[2][t] += a2;
+        __syncthreads();
+    }
+    const unsigned tot2 = sc[2][kOrderThreads - 1], tot1 = sc[1][kOrderThreads - 1];
+    unsigned o2 = sc[2][t] - n2, o1 = tot2 + sc[1][t] - n1, o0 = tot2 + tot1 + sc[0][t] - n0;
+    for (unsigned k = b; k < e; k++) {
+        const unsigned c = cls[k];
+        const unsigned pos = c == 2 ? o2++ : c == 1 ? o1++ : o0++;
+        order[pos] = k;
+    }
+}
+
+hipError_t seg_order_launch(const Params &p, unsigned nseg, unsigned char *cls, unsigned *order, unsigned grid,
+                            size_t lds_bytes, hipStream_t st) {
+    if (nseg == 0) return hipSuccess;
+    grid = std::max(1u, std::min(grid, (nseg + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(seg_class_kernel, dim3(grid), dim3(kBlock), lds_bytes, st, p, nseg, cls);
+    hipLaunchKernelGGL(seg_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, cls, nseg, order);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

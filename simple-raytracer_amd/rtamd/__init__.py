@@ -355,9 +355,11 @@ class GpuScene:
 
     def debug_counters(self) -> list[int]:
         """Raw device counters of the last render (rt_scene_debug_counters)."""
-        buf = (C.c_ulonglong * 48)()
-        rc = hip_lib().rt_scene_debug_counters(self._h, buf, 48)
-        if rc == -1:                  # libraries of rounds 1-2 (A/B baselines) have 32 / 40 slots
+        buf = (C.c_ulonglong * 64)()
+        rc = hip_lib().rt_scene_debug_counters(self._h, buf, 64)
+        if rc == -1:                  # libraries of rounds 1-4 (A/B baselines) have 32 / 40 / 48 slots
+            rc = hip_lib().rt_scene_debug_counters(self._h, buf, 48)
+        if rc == -1:
             rc = hip_lib().rt_scene_debug_counters(self._h, buf, 40)
         if rc == -1:
             rc = hip_lib().rt_scene_debug_counters(self._h, buf, 32)
