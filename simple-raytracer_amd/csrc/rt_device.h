@@ -115,8 +115,6 @@ struct Params {
     unsigned int total;                  // W * rows, or the pixel list's length
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
-    const unsigned *__restrict__ seg_order;   // null, or work item segment k -> segment seg_order[k] (k < seg_full)
-    unsigned seg_full;                   // segments of kSeg work items ordered (the full ones)
     int hot_base, hot_stride;            // copies of the main tree's top (rt_accel.h kHotNodes): the root
     unsigned hot_mask;                   // wave w starts at bvh + hot_base + (w & hot_mask) * hot_stride bytes
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
@@ -177,6 +175,7 @@ static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack -
 #define RT_BLOCK 256                     // lanes per workgroup of render_kernel
 #endif
 constexpr int kBlock = RT_BLOCK;
+constexpr long long kCountTests = 0;     // option count_tests default (the counting kernel is slower)
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /
@@ -213,12 +212,6 @@ constexpr int kStatsReset = kWorkSlots + kWorkStride * kWorkPartsMax;
 constexpr int kStatCopies = 16;
 constexpr int stat_copy_off(int c) { return kWorkSlots + kWorkStride * (c & 7) + 64 + (c >> 3) * 128; }
 static_assert(64 + 128 + kNStats <= kWorkStride, "stat copies fit a band's counter block");
-// Segment order (option order, rt_kernels.hip seg_class_kernel): the work
-// items in segments of kSeg, the full segments handed out in the order of a
-// cost class sampled at item kSegSample of each (its primary hit's material)
-constexpr int kSeg = 64;
-constexpr int kSegSample = 27;           // column 3, row 3 of an 8 x 8 block of an 8-row strip
-constexpr int kOrderThreads = 1024;      // seg_order_kernel: one workgroup
 // Pixels whose shade tree read back() of an empty medium stack (main.cpp:1028,
 // UB in the reference): stats[44] counts the events, the first kUbLogMax
 // pixels follow the work counters as x << 32 | y (rt_scene_debug_ub_pixels)
@@ -239,13 +232,10 @@ int maxf_for_depth(int depth);
 int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes);
 // bytes of one lane's cold ShadeRay frame (Cold<maxf>)
 size_t cold_frame_bytes(int maxf);
-hipError_t render_launch(int maxf, int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st);
-// Segment order for a BVH render of p (p.seg_order / p.seg_full not yet set):
-// classes of nseg full segments into cls, then the stable order (class 2, 1,
-// 0) into order.  grid <= the render's grid (the spill area is the render's);
-// lds_bytes: the traversal stack (stack_cap x kBlock ints).
-hipError_t seg_order_launch(const Params &p, unsigned nseg, unsigned char *cls, unsigned *order, unsigned grid,
-                            size_t lds_bytes, hipStream_t st);
+// tests: the instantiation that counts executed ray-box / face / sphere tests
+// (option count_tests; rt_kernels.hip RT_COUNT)
+hipError_t render_launch(int maxf, int mode, bool tests, const Params &p, unsigned grid, size_t lds_bytes,
+                         hipStream_t st);
 hipError_t deinterleave_launch(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
                                hipStream_t st);
 

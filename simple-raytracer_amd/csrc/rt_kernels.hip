@@ -26,22 +26,24 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "rt_bvh.h"
 #include "rt_device.h"
 
 namespace rt {
 
-// RT_COUNT_TESTS 0: the executed-test counters are compiled out (A/B of their
-// register cost; rt_stats' box/face/sphere tests are then 0)
-#ifndef RT_COUNT_TESTS
-#define RT_COUNT_TESTS 1
-#endif
-#if RT_COUNT_TESTS
-#define RT_COUNT(x) (x)
-#else
-#define RT_COUNT(x) ((void)0)
-#endif
+// Executed-test counters (rt_stats box / face / sphere tests): only in the
+// counting instantiation of the kernel (render_kernel<.., TESTS = true>,
+// option count_tests); in the other one they are compiled out -- their
+// registers, live across the whole loop, cost the traversal.
+// RT_COUNT(x) runs x where a counter object `cnt` of a counting type is in
+// scope; RT_COUNT_IF(on, x) where the switch is a template parameter.
+#define RT_COUNT_IF(on, x) \
+    do {                   \
+        if constexpr (on) { x; } \
+    } while (0)
+#define RT_COUNT(x) RT_COUNT_IF(std::remove_reference_t<decltype(cnt)>::kTests, x)
 
 // Read-only scene data seen through the constant address space: the loads
 // are wave-uniform and invariant, so they become scalar (s_load) reads into
@@ -164,12 +166,12 @@ __device__ __forceinline__ bool sphere_test(float4 s, V3 o, V3 d, float &t1, flo
 
 // The scan every active lane of the wave runs together.  SRC_LDS: primitive
 // arrays were staged into LDS (lds_f, lds_s); otherwise scalar loads.
-template <bool SRC_LDS>
+template <bool SRC_LDS, bool TESTS>
 __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s,
                                      bool part, unsigned &ft, unsigned &st) {
     if (!part) return;
-    RT_COUNT(ft += (unsigned)p.nf);
-    RT_COUNT(st += (unsigned)p.ns);
+    RT_COUNT_IF(TESTS, ft += (unsigned)p.nf);
+    RT_COUNT_IF(TESTS, st += (unsigned)p.ns);
     for (int i = 0; i < p.nf; i++) {
         float4 f0, f1, f2, f3, f4;
         if (SRC_LDS) {
@@ -220,7 +222,9 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 // Per-lane counters kept small (VGPR pressure): ray kinds are counted per
 // wave with ballots in the main loop (scalar registers); only the rare events
 // and the executed-test counts stay per lane.
-struct Counters {
+template <bool TESTS>
+struct CountersT {
+    static constexpr bool kTests = TESTS;
     unsigned skip, ub;
     unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
 #if RT_PROF
@@ -236,7 +240,8 @@ enum RayKind { RK_NONE = 0, RK_SHADOW = 1, RK_REFR = 2, RK_REFL = 3, RK_PRIMARY 
 // Nearest root of object `obj` alone along q with tmin < t < FLT_MAX
 // (kFltMax: none) -- the minimum the reference's in-order scan holds once it
 // has passed that object (main.cpp:997, :1004).
-__device__ __forceinline__ float own_nearest(const Query &q, const Params &p, int obj, Counters &cnt) {
+template <class CNT>
+__device__ __forceinline__ float own_nearest(const Query &q, const Params &p, int obj, CNT &cnt) {
     float tb = kFltMax;
     if (obj < p.nf) {
         const float4 *F = p.fscan + 5 * obj;
@@ -309,8 +314,8 @@ __device__ __forceinline__ float safe_rcp(float x) { return __builtin_amdgcn_rcp
 // opaque occluder there (its other factors are multiplied by the full search
 // that follows, which visits this leaf again); closest and SKIP queries are
 // idempotent under a repeated candidate and run as usual.
-template <bool PRE = false>
-__device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, Counters &cnt, float &best, int &win,
+template <bool PRE = false, class CNT>
+__device__ __forceinline__ void leaf_visit(Query &q, const Params &p, int link, CNT &cnt, float &best, int &win,
                                            bool &opaque, bool faces_only) {
     int v = -link - 1;
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(p.leafrec);
@@ -476,8 +481,8 @@ __device__ __forceinline__ unsigned child_entry(const ChildPlanes &cp, int i, fl
 // query's own ray (q.o, q.d).
 //
 // org_pass: run the origin-leaf pass first (option org_first, by ray kind).
-template <bool point, unsigned LEAF_WAIT = kLeafWait>
-__device__ void bvh_trace(Query &q, const Params &p, int *stk, Counters &cnt, bool org_pass = false, int root = 0,
+template <bool point, unsigned LEAF_WAIT = kLeafWait, class CNT>
+__device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool org_pass = false, int root = 0,
                           V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
     // |1/d| capped at 2^100 (1/0 -> 2^100): the quantised planes'
     // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
@@ -1088,9 +1093,9 @@ __device__ __forceinline__ void ub_note(const Params &p, unsigned pix) {
 }
 
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
-template <int MAXF>
+template <int MAXF, class CNT>
 __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
-                                  bool root, Counters &cnt, unsigned pix) {
+                                  bool root, CNT &cnt, unsigned pix) {
     const int fsn = h_sn(f);
     copy_stack(f, fc, c, root);
     int n = fsn;
@@ -1228,8 +1233,8 @@ __device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d, i
 // until the next TraceRay (returns its kind, RK_SHADOW/RK_REFR/RK_REFL, with q
 // set up) or until the pixel is done (returns RK_NONE with `color` set).
 // Invariant: while a node is on top, q.o is its hit point.
-template <int MAXF>
-__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, Counters &cnt, C3 &color, unsigned pix) {
+template <int MAXF, class CNT>
+__device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt, C3 &color, unsigned pix) {
     const C3 bkg = {p.bkg[0], p.bkg[1], p.bkg[2]};
     int top = ls.top;
     HotR h;
@@ -1452,7 +1457,7 @@ __device__ __forceinline__ V3 primary_dir(const Params &p, int x, int y) {
     return vnorm(vsub(pt, V3{p.eye[0], p.eye[1], p.eye[2]}));
 }
 
-template <int MAXF, int MODE>
+template <int MAXF, int MODE, bool TESTS>
 __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) {
     constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
     // LDS: every lane's shading state (kLdsHot words, kBlock apart), then the
@@ -1475,7 +1480,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     LaneState<MAXF> ls;
     ls.top = -1;
     ls.frames = p.frames;
-    Counters cnt = {0, 0, 0, 0, 0};
+    CountersT<TESTS> cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;
     int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
@@ -1644,9 +1649,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                     unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
                     unsigned idx = rank < split ? base + rank : nbase + (rank - split);
                     if (idx < (rank < split ? old_end : new_end)) {
-                        // option order: the k-th full segment handed out is seg_order[k]
-                        if (p.seg_order && idx / (unsigned)kSeg < p.seg_full)
-                            idx = p.seg_order[idx / (unsigned)kSeg] * (unsigned)kSeg + idx % (unsigned)kSeg;
                         int px, py;
                         pixel_xy(p, idx, px, py);
                         q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
@@ -1762,12 +1764,12 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             bool need = search && q.bf;
             const unsigned long long nb = __ballot(need);
             w_bf += (unsigned)__popcll(nb);
-            if (nb) scan<false>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
+            if (nb) scan<false, TESTS>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
 #if RT_PROF
             pc_bf += __builtin_amdgcn_s_memtime() - c2;
 #endif
         } else {
-            scan<SRC_LDS>(q, p, lds_f, lds_s, search, cnt.ftests, cnt.stests);
+            scan<SRC_LDS, TESTS>(q, p, lds_f, lds_s, search, cnt.ftests, cnt.stests);
         }
     }
     unsigned long long *st = p.stats;
@@ -1784,9 +1786,11 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     }
     atomicAdd(&sc[4], (unsigned long long)cnt.skip);
     atomicAdd(&sc[5], (unsigned long long)cnt.ub);
-    atomicAdd(&sc[6], (unsigned long long)cnt.boxes);
-    atomicAdd(&sc[7], (unsigned long long)cnt.ftests);
-    atomicAdd(&sc[8], (unsigned long long)cnt.stests);
+    if constexpr (TESTS) {
+        atomicAdd(&sc[6], (unsigned long long)cnt.boxes);
+        atomicAdd(&sc[7], (unsigned long long)cnt.ftests);
+        atomicAdd(&sc[8], (unsigned long long)cnt.stests);
+    }
 #endif
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
@@ -1856,98 +1860,6 @@ __global__ void deinterleave_kernel(const float *__restrict__ gathered, int worl
 }
 
 // ---------------------------------------------------------------------------
-// Segment order (option order): the costliest work first
-// ---------------------------------------------------------------------------
-// A frame lasts until its last pixel is done, and pixels differ by two orders
-// of magnitude: one whose primary ray meets glass opens a tree of up to
-// 2^depth refraction and reflection nodes, ~100 traces one after the other in
-// its lane, while a diffuse pixel takes 3.  Handed out in image order, the
-// costly pixels of the last work items set the frame's tail (C3: the last
-// ~1.1 ms of 13 with fewer and fewer waves alive; at N = 8 half of a rank's
-// frame, profiles/r04/timeline_*.json).  Longest first: the full segments of
-// kSeg work items go out by a cost class sampled at one item each -- its
-// primary ray's nearest object: 2 refracting (opacity < 1, eta > 0, the test
-// of the shading code), 1 reflecting (ks > 0), 0 anything else or a miss --
-// class 2 first, in image order within a class.  Which lane renders which
-// pixel when changes; no pixel does.
-__global__ void __launch_bounds__(kBlock) seg_class_kernel(Params p, unsigned nseg, unsigned char *__restrict__ cls) {
-    int *stk = reinterpret_cast<int *>(rt_lds) + threadIdx.x;   // the traversal stack, entries kBlock apart
-    stk[0] = rtbvh::kEmpty;
-    Counters cnt = {0, 0, 0, 0, 0};
-    for (unsigned k = blockIdx.x * kBlock + threadIdx.x; k < nseg; k += gridDim.x * kBlock) {
-        int px, py;
-        pixel_xy(p, k * (unsigned)kSeg + (unsigned)kSegSample, px, py);
-        Query q;
-        q.o = V3{p.eye[0], p.eye[1], p.eye[2]};
-        q.d = primary_dir(p, px, py);
-        q.tmin = 0.0f;
-        q.tmax = kFltMax;
-        q.unb = false;
-        q.self = -1;
-        q.back = -1;
-        q.win = -1;
-        q.closest = true;
-        q.skipchk = q.skipped = q.bf = false;
-        q.mask = 1.0f;
-        bvh_trace<false>(q, p, stk, cnt);
-        unsigned char c = 0;
-        if (q.win >= 0) {
-            const ObjK &o = p.objs[q.win];
-            c = ((double)o.opacity < 1.0 && o.eta > 0) ? 2 : (double)o.ks > 0.0 ? 1 : 0;
-        }
-        cls[k] = c;
-    }
-}
-
-// Stable counting sort of the segments by class (2, 1, 0) in one workgroup:
-// thread t counts its contiguous run of segments, a scan over the threads
-// gives each run its offsets, and each thread writes its run in order.
-__global__ void __launch_bounds__(kOrderThreads) seg_order_kernel(const unsigned char *__restrict__ cls, unsigned nseg,
-                                                                 unsigned *__restrict__ order) {
-    __shared__ unsigned sc[3][kOrderThreads];
-    const unsigned t = threadIdx.x;
-    const unsigned per = (nseg + kOrderThreads - 1) / kOrderThreads;
-    const unsigned b = min(nseg, t * per), e = min(nseg, b + per);
-    unsigned n0 = 0, n1 = 0, n2 = 0;
-    for (unsigned k = b; k < e; k++) {
-        const unsigned c = cls[k];
-        n0 += c == 0;
-        n1 += c == 1;
-        n2 += c == 2;
-    }
-    sc[0][t] = n0;
-    sc[1][t] = n1;
-    sc[2][t] = n2;
-    __syncthreads();
-    // inclusive scan over the threads (Hillis-Steele), each class
-    for (unsigned d = 1; d < kOrderThreads; d <<= 1) {
-        unsigned a0 = 0, a1 = 0, a2 = 0;
-        if (t >= d) a0 = sc[0][t - d], a1 = sc[1][t - d], a2 = sc[2][t - d];
-        __syncthreads();
-        sc[0][t] += a0;
-        sc[1][t] += a1;
-        sc[2][t] += a2;
-        __syncthreads();
-    }
-    const unsigned tot2 = sc[2][kOrderThreads - 1], tot1 = sc[1][kOrderThreads - 1];
-    unsigned o2 = sc[2][t] - n2, o1 = tot2 + sc[1][t] - n1, o0 = tot2 + tot1 + sc[0][t] - n0;
-    for (unsigned k = b; k < e; k++) {
-        const unsigned c = cls[k];
-        const unsigned pos = c == 2 ? o2++ : c == 1 ? o1++ : o0++;
-        order[pos] = k;
-    }
-}
-
-hipError_t seg_order_launch(const Params &p, unsigned nseg, unsigned char *cls, unsigned *order, unsigned grid,
-                            size_t lds_bytes, hipStream_t st) {
-    if (nseg == 0) return hipSuccess;
-    grid = std::max(1u, std::min(grid, (nseg + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL(seg_class_kernel, dim3(grid), dim3(kBlock), lds_bytes, st, p, nseg, cls);
-    hipLaunchKernelGGL(seg_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, cls, nseg, order);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // Launch interface (rt_device.h)
 // ---------------------------------------------------------------------------
 int maxf_for_depth(int depth) {
@@ -1962,7 +1874,8 @@ size_t cold_frame_bytes(int maxf) {
 template <int MAXF, int MODE>
 static int blocks_one(size_t lds_bytes) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE>, kBlock, lds_bytes) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE, false>, kBlock, lds_bytes) !=
+        hipSuccess)
         return 0;
     return nb;
 }
@@ -1980,22 +1893,29 @@ int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes) {
     return blocks_mode<17>(mode, lds_bytes);
 }
 
-template <int MAXF>
+template <int MAXF, bool TESTS>
 static hipError_t launch_mode(int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st) {
     if (mode == MODE_BVH)
-        hipLaunchKernelGGL((render_kernel<MAXF, MODE_BVH>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
+        hipLaunchKernelGGL((render_kernel<MAXF, MODE_BVH, TESTS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
     else if (mode == MODE_SCAN_LDS)
-        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN_LDS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
+        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN_LDS, TESTS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
     else
-        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
+        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN, TESTS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
     return hipGetLastError();
 }
 
-hipError_t render_launch(int maxf, int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st) {
-    if (maxf == 5) return launch_mode<5>(mode, p, grid, lds_bytes, st);
-    if (maxf == 9) return launch_mode<9>(mode, p, grid, lds_bytes, st);
-    if (maxf == 17) return launch_mode<17>(mode, p, grid, lds_bytes, st);
+template <bool TESTS>
+static hipError_t launch_maxf(int maxf, int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st) {
+    if (maxf == 5) return launch_mode<5, TESTS>(mode, p, grid, lds_bytes, st);
+    if (maxf == 9) return launch_mode<9, TESTS>(mode, p, grid, lds_bytes, st);
+    if (maxf == 17) return launch_mode<17, TESTS>(mode, p, grid, lds_bytes, st);
     return hipErrorInvalidValue;
+}
+
+hipError_t render_launch(int maxf, int mode, bool tests, const Params &p, unsigned grid, size_t lds_bytes,
+                         hipStream_t st) {
+    return tests ? launch_maxf<true>(maxf, mode, p, grid, lds_bytes, st)
+                 : launch_maxf<false>(maxf, mode, p, grid, lds_bytes, st);
 }
 
 hipError_t deinterleave_launch(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,

@@ -75,7 +75,7 @@ struct rt_scene {
     AccelInput in;                     // host arrays + BVH sources (rt_accel.h)
     long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
     long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
-    long long opt_order = -1;          // segment order: -1 auto (scenes with secondary rays), 0 off, 1 on
+    long long opt_count_tests = kCountTests;   // 1: count executed ray-box / face / sphere tests
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
     float4 *d_leafrec = nullptr;
@@ -90,7 +90,7 @@ struct rt_scene {
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
     long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0, last_work_parts = 0;
-    long long last_hot_copies = 0, last_ordered = 0;
+    long long last_hot_copies = 0;
     long long bvh_nodes = 0;
     bool last_valid = false;
 };
@@ -170,24 +170,13 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     pl.refill_min = refill_for(s, pl);
     // work bands: one per XCD (workgroup b runs on XCD b mod 8: its L2), unless
     // the launch is too small to give each band a workgroup (option work_parts)
-    // segment order (option order, rt_kernels.hip seg_class_kernel): BVH
-    // renders of scenes whose pixels open refraction / reflection trees --
-    // elsewhere every pixel costs about the same
-    const unsigned nseg = p.total / (unsigned)kSeg;
-    const bool ordered = mode == MODE_BVH && !p.pix && nseg > 0 &&
-                         (s->opt_order > 0 || (s->opt_order < 0 && s->secondary && p.depth > 0));
-    // (its costly segments come first in the order: one band, not one per XCD)
     const unsigned parts = s->opt_work_parts > 0 ? (unsigned)s->opt_work_parts
-                           : (!ordered && grid >= kWorkPartsMax && p.total >= (unsigned)(kWorkPartsMax * kBlock))
+                           : (grid >= kWorkPartsMax && p.total >= (unsigned)(kWorkPartsMax * kBlock))
                                ? (unsigned)kWorkPartsMax
                                : 1u;
     pl.work_shift = parts >= 8 ? 3 : parts >= 4 ? 2 : parts >= 2 ? 1 : 0;
     const size_t cold_bytes = (size_t)grid * kBlock * maxf * cold_frame_bytes(maxf);
-    const size_t ovf_bytes = (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
-    auto up256 = [](size_t v) { return (v + 255) / 256 * 256; };
-    const size_t cls_off = up256(cold_bytes + ovf_bytes);
-    const size_t order_off = up256(cls_off + (ordered ? nseg : 0));
-    size_t fbytes = ordered ? order_off + (size_t)nseg * sizeof(unsigned) : cold_bytes + ovf_bytes;
+    size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
@@ -210,20 +199,8 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     s->last_stack_cap = pl.stack_cap;
     s->last_lights_in_lds = pl.lights_in_lds;
     s->last_work_parts = 1 << pl.work_shift;
-    s->last_ordered = ordered ? 1 : 0;
     if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
-    pl.seg_order = nullptr;
-    pl.seg_full = 0;
-    if (ordered) {
-        unsigned char *cls = static_cast<unsigned char *>(slot.d_frames) + cls_off;
-        unsigned *order = reinterpret_cast<unsigned *>(static_cast<char *>(slot.d_frames) + order_off);
-        const hipError_t e =
-            seg_order_launch(pl, nseg, cls, order, (unsigned)grid, (size_t)pl.stack_cap * kBlock * sizeof(int), st);
-        if (e != hipSuccess) return e;
-        pl.seg_order = order;
-        pl.seg_full = nseg;
-    }
-    return render_launch(maxf, mode, pl, (unsigned)grid, shm, st);
+    return render_launch(maxf, mode, s->opt_count_tests != 0, pl, (unsigned)grid, shm, st);
 }
 
 // (Re)build the BVH for distance bound D on the host (rt_accel.cpp) and
@@ -613,9 +590,9 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         else s->opt_bvh_node = std::max(0LL, value);
         s->bvh_D = -1.0;               // rebuild on the next render
     }
-    else if (k == "order") {
-        if (value < -1 || value > 1) return RT_E_INVALID;
-        s->opt_order = value;
+    else if (k == "count_tests") {
+        if (value < 0 || value > 1) return RT_E_INVALID;
+        s->opt_count_tests = value;
     }
     else if (k == "hot_copies") {
         if (value < 0 || value > 64 || (value & (value - 1))) return RT_E_INVALID;
@@ -802,7 +779,7 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[43] = (unsigned long long)s->last_lights_in_lds;
     h[45] = (unsigned long long)s->last_work_parts;
     h[44] = (unsigned long long)s->last_hot_copies;
-    h[48] = (unsigned long long)s->last_ordered;
+    h[48] = (unsigned long long)s->opt_count_tests;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }
