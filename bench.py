@@ -73,6 +73,10 @@ def parse_args():
                          "the multi-rank data path on one GPU (ranks share device 0)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the last gathered image bit for bit against one whole-image render")
+    ap.add_argument("--gather-format", default="auto", choices=["auto", "f32", "u8"],
+                    help="N>1: what rank 0 gathers -- f32 rows (12 B per pixel) or the P3 writer's "
+                         "pixel values as bytes (3 B, quantised on each rank's GPU; exact for values "
+                         "0..255). auto = u8 unless the warm-up frame has a value outside 0..255")
     ap.add_argument("--out-json", default=None)
     return ap.parse_args()
 
@@ -225,7 +229,8 @@ def main() -> None:
     if F > 1:
         gs.set_option("inflight", F)
     gs.prepare(cam, W, H)                 # BVH + every slot's frame buffer, before any step
-    gathers = [ImageGather(H, W, world, rank, "cuda", torch) for _ in range(F)]
+    fmt = "f32" if world == 1 or args.gather_format == "f32" else "u8"
+    gathers = [ImageGather(H, W, world, rank, "cuda", torch, fmt) for _ in range(F)]
     streams = [torch.cuda.Stream() for _ in range(F)]
     for s in streams:                     # bind each stream to its hardware queue before timing
         with torch.cuda.stream(s):
@@ -240,9 +245,29 @@ def main() -> None:
                                            s.cuda_stream)
             return g.gather(dist)
 
-    for k in range(args.warmup):
+    def any_flag() -> bool:
+        # a value outside 0..255 on any rank (u8 gathers): the bytes are not the writer's
+        f = torch.zeros(1, dtype=torch.int32, device="cuda")
+        for g in gathers:
+            if g.flag is not None:
+                f |= g.flag
+        if world > 1:
+            ff = f if args.dist_backend == "nccl" else f.cpu()
+            dist.all_reduce(ff, op=dist.ReduceOp.MAX)
+            f = ff
+        return bool(int(f.item()))
+
+    for k in range(max(1, args.warmup)):
         step(k)
     torch.cuda.synchronize()
+    if fmt == "u8" and any_flag():
+        if args.gather_format == "u8":
+            raise SystemExit("--gather-format u8: the image has values outside 0..255")
+        fmt = "f32"
+        gathers = [ImageGather(H, W, world, rank, "cuda", torch, fmt) for _ in range(F)]
+        for k in range(max(1, args.warmup)):
+            step(k)
+        torch.cuda.synchronize()
 
     if world > 1:
         dist.barrier()
@@ -254,6 +279,8 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if fmt == "u8" and any_flag():     # the frames are identical: cannot differ from the warm-up's
+        raise SystemExit("u8 gather: a timed frame had values outside 0..255")
     verified = None
     if args.verify and rank == 0:
         # the last timed step's image (all ranks' rows, gathered and put back in
@@ -262,8 +289,14 @@ def main() -> None:
         vs = rtamd.GpuScene(hs, device=dev)
         vs.render_rows_async(cam, W, H, 0, H, ref.data_ptr(), torch.cuda.current_stream().cuda_stream)
         vs.last_stats()
+        if fmt == "u8":                   # the gathered bytes against the whole render's
+            from rtamd.dist import quantize_u8_device
+            ref8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+            flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+            quantize_u8_device(rtamd, torch, ref, ref8, flag)
+            ref = ref8
         torch.cuda.synchronize()
-        a, b = torch.nan_to_num(last_img, nan=-9.0), torch.nan_to_num(ref, nan=-9.0)
+        a, b = torch.nan_to_num(last_img.float(), nan=-9.0), torch.nan_to_num(ref.float(), nan=-9.0)
         verified = bool(torch.equal(a, b))
         vs.close()
         if not verified:
@@ -364,6 +397,8 @@ def main() -> None:
                        "rays_per_step": int(rays_total), "parallelism": f"interleaved 8-row blocks x{world}"
                        + ((" + RCCL gather" if args.dist_backend == "nccl" else " + gloo gather (rehearsal, one GPU)")
                           if world > 1 else ""), "frames_in_flight": F,
+                       "gather_format": (fmt + (" (the P3 writer's values, 3 B/pixel)" if fmt == "u8" else
+                                                " (12 B/pixel)")) if world > 1 else None,
                        "reserved_block_slots": reserve,
                        "launch": {"blocks_per_cu": int(dbg[17]), "grid": int(dbg[18]),
                                   "lds_bytes_per_block": int(dbg[19]), "bvh_nodes": int(dbg[20]),

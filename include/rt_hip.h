@@ -192,6 +192,15 @@ int rt_render_pixels(rt_scene *scene, const rt_camera *cam, int W, int H, const 
 int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
                          void *hip_stream);
 
+/* The P3 writer's pixel values (main.cpp:760, rth_quantize) of n floats as
+ * bytes, on the device: out[i] = (int)(rgb[i] * 255) when that is 0..255;
+ * otherwise (NaN, values above 1 or below 0 -- the writer prints those as
+ * other integers) out[i] = 0 and bit 0 of *flag is set, and the caller must
+ * keep the floats.  rgb 16-byte, out 4-byte aligned, device memory;
+ * asynchronous on hip_stream.  A multi-GPU render gathers these 3 bytes per
+ * pixel instead of 12 (rtamd/dist.py ImageGather, bench.py). */
+int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *flag, void *hip_stream);
+
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
  * (persistent blocks, 0 = occupancy), "reserve" (block slots the occupancy-

@@ -232,6 +232,8 @@ int maxf_for_depth(int depth);
 int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes);
 // bytes of one lane's cold ShadeRay frame (Cold<maxf>)
 size_t cold_frame_bytes(int maxf);
+// rt_quantize_u8 (rgb: n floats, 16-B aligned; out: n bytes, 4-B aligned)
+hipError_t quantize_u8_launch(const float *rgb, size_t n, unsigned char *out, unsigned *flag, hipStream_t st);
 // tests: the instantiation that counts executed ray-box / face / sphere tests
 // (option count_tests; rt_kernels.hip RT_COUNT)
 hipError_t render_launch(int maxf, int mode, bool tests, const Params &p, unsigned grid, size_t lds_bytes,

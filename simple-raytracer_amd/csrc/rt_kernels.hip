@@ -1859,6 +1859,42 @@ __global__ void deinterleave_kernel(const float *__restrict__ gathered, int worl
         dst[i] = src[i];
 }
 
+// The P3 writer's values (main.cpp:760: (size_t)(int)(c * 255), rth_quantize)
+// as bytes, for a gather of 3 B instead of 12 per pixel: a value is stored as
+// its byte when the writer's value is 0..255 -- c * 255 in (-1, 256), where
+// the truncation gives 0..255 -- and otherwise (NaN, a background above 1,
+// a negative colour) *flag gets bit 0 and the byte is 0: the caller must then
+// use the floats.  Four values per thread (float4 in, 4 bytes out).
+__global__ void quantize_u8_kernel(const float4 *__restrict__ rgb, size_t n4, const float *__restrict__ tail,
+                                   size_t ntail, unsigned *__restrict__ out, unsigned char *__restrict__ out_tail,
+                                   unsigned *__restrict__ flag) {
+    auto q1 = [](float c, bool &bad) -> unsigned {
+        const float x = c * 255.0f;                  // (c - 0) * (255 - 0) / (1 - 0) + 0, exactly
+        const bool ok = (x > -1.0f) & (x < 256.0f);  // false for NaN
+        bad |= !ok;
+        return ok ? (unsigned)(int)x : 0u;
+    };
+    bool bad = false;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n4) {
+        const float4 v = rgb[i];
+        out[i] = q1(v.x, bad) | (q1(v.y, bad) << 8) | (q1(v.z, bad) << 16) | (q1(v.w, bad) << 24);
+    }
+    if (i < ntail) out_tail[i] = (unsigned char)q1(tail[i], bad);
+    if (__ballot(bad) && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(bad)) - 1))
+        atomicOr(flag, 1u);
+}
+
+hipError_t quantize_u8_launch(const float *rgb, size_t n, unsigned char *out, unsigned *flag, hipStream_t st) {
+    const size_t n4 = n / 4, ntail = n % 4;
+    const size_t threads = std::max<size_t>(n4, ntail);
+    if (threads == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    hipLaunchKernelGGL(quantize_u8_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float4 *>(rgb), n4,
+                       rgb + 4 * n4, ntail, reinterpret_cast<unsigned *>(out), out + 4 * n4, flag);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Launch interface (rt_device.h)
 // ---------------------------------------------------------------------------

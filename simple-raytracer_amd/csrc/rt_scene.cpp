@@ -679,6 +679,12 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
                : RT_E_HIP;
 }
 
+int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *flag, void *hip_stream) {
+    if (!rgb || !out || !flag || n < 0) return RT_E_INVALID;
+    if ((reinterpret_cast<uintptr_t>(rgb) & 15) || (reinterpret_cast<uintptr_t>(out) & 3)) return RT_E_INVALID;
+    return quantize_u8_launch(rgb, (size_t)n, out, flag, (hipStream_t)hip_stream) == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
 int rt_scene_prepare(rt_scene *s, const rt_camera *cam, int W, int H) {
     if (!s || !cam || W < 2 || H < 2) return RT_E_INVALID;
     if ((long long)W * H >= (1ll << 31)) return RT_E_UNSUPPORTED;

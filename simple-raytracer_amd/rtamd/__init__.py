@@ -91,7 +91,7 @@ HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_ren
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_scene_debug_ub_pixels",
-               "rt_deinterleave_rows",
+               "rt_deinterleave_rows", "rt_quantize_u8",
                "rt_strerror"]
 
 
@@ -161,6 +161,8 @@ def hip_lib() -> C.CDLL:
         if hasattr(L, "rt_deinterleave_rows"):
             L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                C.c_void_p, C.c_void_p]
+        if hasattr(L, "rt_quantize_u8"):           # absent from round-1..3 libraries (A/B baselines)
+            L.rt_quantize_u8.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
         L.rt_strerror.restype = C.c_char_p
@@ -250,6 +252,13 @@ def quantize(rgb: np.ndarray) -> np.ndarray:
     out = np.empty(a.shape, dtype=np.int64)
     host_lib().rth_quantize(a.ctypes.data, a.size, out.ctypes.data)
     return out
+
+
+def quantize_u8_device(rgb_ptr: int, n: int, out_ptr: int, flag_ptr: int, stream: int = 0) -> None:
+    """rt_quantize_u8 on device buffers: the P3 writer's values of n floats
+    as bytes; bit 0 of the uint32 at flag_ptr is set when a value is not 0..255."""
+    _check(hip_lib().rt_quantize_u8(C.c_void_p(rgb_ptr), n, C.c_void_p(out_ptr), C.c_void_p(flag_ptr),
+                                    C.c_void_p(stream)), "rt_quantize_u8")
 
 
 def write_ppm(path: str, rgb: np.ndarray, threads: int = 0) -> None:

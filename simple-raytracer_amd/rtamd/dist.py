@@ -31,17 +31,31 @@ def image_rows(H: int, world: int, rank: int, block: int = BLOCK) -> list[int]:
 class ImageGather:
     """One frame's row buffer on this rank plus, on rank 0, the gather targets,
     the full image and the image-order row indices (built once, reused every
-    frame: no host->device index copies in the frame loop)."""
+    frame: no host->device index copies in the frame loop).
 
-    def __init__(self, H: int, W: int, world: int, rank: int, device, torch):
+    fmt "f32" gathers the float rows (12 B per pixel); "u8" gathers the P3
+    writer's pixel values as bytes (3 B per pixel; rt_quantize_u8 on the
+    device, exact for values 0..255).  A value outside 0..255 (NaN, a
+    background above 1) sets `self.flag` on the device: the u8 image is then
+    not the writer's, and the caller must use "f32" (bench.py decides from its
+    warm-up frame and checks the flag after the timed ones)."""
+
+    def __init__(self, H: int, W: int, world: int, rank: int, device, torch, fmt: str = "f32"):
         *_, rows_per = row_set(H, world, rank)
-        self.H, self.world, self.rank, self.torch = H, world, rank, torch
+        self.H, self.world, self.rank, self.torch, self.fmt = H, world, rank, torch, fmt
         self.strip = torch.zeros((rows_per, W, 3), dtype=torch.float32, device=device)
+        self.send = self.strip
+        self.flag = None
+        if fmt == "u8":
+            self.send = torch.zeros((rows_per, W, 3), dtype=torch.uint8, device=device)
+            self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        elif fmt != "f32":
+            raise ValueError(f"gather format {fmt!r}")
         self.targets = self.image = None
         self.index = []
         if world > 1 and rank == 0:
-            self.targets = [torch.empty_like(self.strip) for _ in range(world)]
-            self.image = torch.empty((H, W, 3), dtype=torch.float32, device=device)
+            self.targets = [torch.empty_like(self.send) for _ in range(world)]
+            self.image = torch.empty((H, W, 3), dtype=self.send.dtype, device=device)
             for r in range(world):
                 rows = image_rows(H, world, r)
                 self.index.append(torch.tensor(rows, dtype=torch.long, device=device) if rows else None)
@@ -50,18 +64,21 @@ class ImageGather:
         """Collect every rank's rows on rank 0 (one fixed-count collective) and
         put them in image order; returns the H x W x 3 image there (None
         elsewhere)."""
+        if self.fmt == "u8":
+            import rtamd
+            quantize_u8_device(rtamd, self.torch, self.strip, self.send, self.flag)
         if self.world == 1:
-            return self.strip[: self.H]
-        if self.strip.is_cuda and dist.get_backend() == "gloo":
+            return self.send[: self.H]
+        if self.send.is_cuda and dist.get_backend() == "gloo":
             # gloo (rehearsal of the multi-rank path on one GPU): host staging
-            cpu = self.strip.cpu()
+            cpu = self.send.cpu()
             tg = [self.torch.empty_like(cpu) for _ in range(self.world)] if self.rank == 0 else None
             dist.gather(cpu, tg, dst=0)
             if self.rank == 0:
                 for r in range(self.world):
                     self.targets[r].copy_(tg[r])
         else:
-            dist.gather(self.strip, self.targets, dst=0)
+            dist.gather(self.send, self.targets, dst=0)
         if self.rank != 0:
             return None
         for r, idx in enumerate(self.index):
@@ -69,3 +86,12 @@ class ImageGather:
                 self.image.index_copy_(0, idx, self.targets[r][: idx.numel()])
         return self.image
 
+
+
+def quantize_u8_device(rtamd, torch, rgb, out, flag) -> None:
+    """rt_quantize_u8 of a float32 device tensor into a uint8 one of the same
+    shape, on the current stream (bit 0 of flag: a value outside 0..255)."""
+    assert rgb.is_cuda and rgb.dtype == torch.float32 and out.dtype == torch.uint8
+    assert rgb.is_contiguous() and out.is_contiguous() and rgb.numel() == out.numel()
+    rtamd.quantize_u8_device(rgb.data_ptr(), rgb.numel(), out.data_ptr(), flag.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)

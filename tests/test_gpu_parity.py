@@ -1012,11 +1012,43 @@ def test_cli_rccl_gather_multi_device(tmp_path):
     assert np.array_equal(np.nan_to_num(outs["host"][1], nan=-9), np.nan_to_num(outs["rccl"][1], nan=-9))
 
 
-def test_multi_rank_hip_path_gloo():
+def test_quantize_u8_device():
+    """rt_quantize_u8 (the gather's 3-byte pixels) equals the P3 writer's
+    values (rth_quantize, main.cpp:760) wherever those are 0..255, and flags
+    every other value -- NaN, infinities, above 1, at or below -1/255 -- on
+    random colours and the boundaries, for lengths that are and are not
+    multiples of 4."""
+    torch = pytest.importorskip("torch")
+    from rtamd.dist import quantize_u8_device
+    rng = np.random.default_rng(7)
+    edge = np.array([0.0, -0.0, 1.0, 0.5, 1 / 255, 254.999 / 255, 255.999 / 255, -0.5 / 255,
+                     -0.999 / 255, np.nextafter(np.float32(-1 / 255), np.float32(0)), 1e-30, -1e-30],
+                    dtype=np.float32)
+    bad = np.array([np.nan, np.inf, -np.inf, 1.5, 256 / 255, -1 / 255, -2.0, 3e9], dtype=np.float32)
+    for n in (1, 3, 4, 7, 1000, 4099):
+        good = np.concatenate([edge, rng.random(n, dtype=np.float32)])[:max(n, 1)]
+        for vals, expect_flag in ((good, False), (np.concatenate([good, bad[: 1 + n % len(bad)]]), True)):
+            ref = rtamd.quantize(vals.reshape(-1))
+            x = torch.from_numpy(vals.copy()).cuda()
+            out = torch.full((vals.size,), 77, dtype=torch.uint8, device="cuda")
+            flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+            quantize_u8_device(rtamd, torch, x, out, flag)
+            torch.cuda.synchronize()
+            o = out.cpu().numpy().astype(np.int64)
+            inr = (ref >= 0) & (ref <= 255)
+            assert np.array_equal(o[inr], ref[inr]), n
+            assert (o[~inr] == 0).all()
+            assert inr.all() != expect_flag, (n, ref[~inr])        # the host writer agrees on the cases
+            assert bool(flag.item() & 1) == expect_flag, n
+
+
+@pytest.mark.parametrize("fmt", ["f32", "auto"])
+def test_multi_rank_hip_path_gloo(fmt):
     """The N > 1 bench data path with the HIP renderer (not the oracle): two
     ranks on one GPU (gloo gather staged through the host), each rendering
     its interleaved row set; rank 0 checks the gathered image bit for bit
-    against one whole-image render (bench.py --verify)."""
+    against one whole-image render (bench.py --verify) -- float rows, and
+    (auto) the P3 writer's values as bytes, quantised on each rank."""
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -1025,12 +1057,13 @@ def test_multi_rank_hip_path_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
            "--gpus", "2", "--dist-backend", "gloo", "--verify", "--steps", "2", "--warmup", "1",
-           "--config", "C2", "--cpu-baseline", "off"]
+           "--config", "C2", "--cpu-baseline", "off", "--gather-format", fmt]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["verified"] is True and line["n_gpus"] == 2
-    _summary["multi_rank_gloo_C2"] = dict(value=line["value"], verified=line["verified"])
+    assert line["config"]["gather_format"].startswith("f32" if fmt == "f32" else "u8"), line["config"]
+    _summary[f"multi_rank_gloo_C2_{fmt}"] = dict(value=line["value"], verified=line["verified"])
 
 
 def test_bvh_upload_failure_leaves_no_stale_tree():

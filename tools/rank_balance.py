@@ -8,7 +8,7 @@ the ranks do not slow each other down (each has its own GPU) and adds the
 RCCL gather's xGMI time estimate (strip bytes / 153 GB/s per link, SURVEY.md
 §8e).  PROJECTED, not measured on N GPUs.
 
-  python tools/rank_balance.py C3 [--frames 8] [--inflight 8] [--reserve 8]
+  python tools/rank_balance.py C3 [--frames 64] [--inflight 8] [--reserve 8]
 """
 from __future__ import annotations
 
@@ -28,7 +28,10 @@ XGMI_GBPS = 153.0          # one xGMI link, per direction
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config", nargs="?", default="C3")
-    ap.add_argument("--frames", type=int, default=8)
+    # frames per pipelined measurement: bench.py times 300 steps, so its last
+    # frame's tail and its first frame's ramp are spread over 300; 8 frames
+    # (round 3) charged each frame 1/8 of them
+    ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--inflight", type=int, default=8)
     ap.add_argument("--reserve", type=int, default=8)
     ap.add_argument("--ns", default="1,2,4,8")
