@@ -83,6 +83,19 @@ def main():
     out = {"config": a.config, "imsize": [W, H], "frames": a.frames, "inflight": a.inflight,
            "reserve": a.reserve, "options": a.option, "note": "PROJECTED from one GPU: each rank's row set rendered alone; "
                                           "not measured on N GPUs", "n": {}}
+    # what bench.py gathers at N > 1 (--gather-format auto): the P3 writer's
+    # values as bytes unless the image has a value outside 0..255
+    from rtamd.dist import quantize_u8_device
+    whole = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    alone.render_row_blocks_async(cam, W, H, 0, H, H, H, whole.data_ptr())
+    alone.last_stats()
+    q8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    quantize_u8_device(rtamd, torch, whole, q8, flag)
+    torch.cuda.synchronize()
+    bpp = 4 if int(flag.item()) else 1
+    out["gather_format"] = "f32" if bpp == 4 else "u8"
+    del whole, q8
     base = None
     for n in (int(v) for v in a.ns.split(",")):
         ranks = []
@@ -98,7 +111,7 @@ def main():
         rays = sum(x["rays"] for x in ranks)
         k = [x["kernel_ms"] for x in ranks]
         p = [x["pipelined_ms"] for x in ranks]
-        strip_bytes = row_set(H, n, 0)[4] * W * 3 * 4
+        strip_bytes = row_set(H, n, 0)[4] * W * 3 * bpp
         gather_ms = strip_bytes / (XGMI_GBPS * 1e9) * 1e3 if n > 1 else 0.0
         step_ms = max(p) + gather_ms           # the gather of frame k overlaps frame k+1 only partly: counted whole
         ent = dict(ranks=ranks, kernel_ms_max=max(k), kernel_ms_mean=round(sum(k) / n, 3),
