@@ -12,3 +12,5 @@ timeout -k 10 500 python -u tools/ab.py --rounds 3 --steps 20 --config C3 def: c
 timeout -k 10 300 python -u tools/ab.py --rounds 2 --steps 3 --config C5 def: ct1::count_tests=1 ns:lib_nostats: > $O/ab_C5.txt 2>&1
 timeout -k 10 300 python -u tools/ab.py --rounds 2 --steps 20 --config C4 def: ct1::count_tests=1 ns:lib_nostats: > $O/ab_C4.txt 2>&1
 timeout -k 10 200 python -u bench.py --steps 20 > $O/bench_C3.json 2> $O/bench_C3.err
+timeout -k 10 300 python -u tools/rank_balance.py C3 > $O/rb_C3.txt 2>&1
+timeout -k 10 300 python -u tools/rank_balance.py C4 > $O/rb_C4.txt 2>&1
