@@ -115,6 +115,7 @@ struct Params {
     unsigned int total;                  // W * rows, or the pixel list's length
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
+    int last_light_skip;                 // a last light with a Phong sum of 0 is not searched (advance)
     int hot_base, hot_stride;            // copies of the main tree's top (rt_accel.h kHotNodes): the root
     unsigned hot_mask;                   // wave w starts at bvh + hot_base + (w & hot_mask) * hot_stride bytes
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)

@@ -1229,6 +1229,17 @@ __device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d, i
     q.win = -1;
 }
 
+// A light's diffuse + specular sum for light direction L (main.cpp:930-950)
+__device__ __forceinline__ C3 phong_sum(const HotR &h, const ObjK &ob, V3 L) {
+    // H only feeds the specular power: rsqrt instead of 3 IEEE divisions
+    // (<= 2 ulp; vnorm(0) = NaN either way)
+    V3 hv = vadd(L, h.I);
+    V3 H = vmul(hv, __builtin_amdgcn_rsqf(vdot(hv, hv)));
+    C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
+    C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
+    return cadd(dc, sc);
+}
+
 // Advance one lane after its scan: consume the result, run ShadeRay logic
 // until the next TraceRay (returns its kind, RK_SHADOW/RK_REFR/RK_REFL, with q
 // set up) or until the pixel is done (returns RK_NONE with `color` set).
@@ -1265,17 +1276,11 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             // that ray's direction for a point light, the constant -L for a
             // directional one (q.d is not modified by a trace)
             V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
-            // H only feeds the specular power: rsqrt instead of 3 IEEE
-            // divisions (<= 2 ulp; vnorm(0) = NaN either way)
-            V3 hv = vadd(L, h.I);
-            V3 H = vmul(hv, __builtin_amdgcn_rsqf(vdot(hv, hv)));
-            C3 dc = cmulf(cmulf(h.dif, ob.kd), max0(vdot(h.N, L)));
-            C3 sc = cmulf(cmulf(C3{ob.spc[0], ob.spc[1], ob.spc[2]}, ob.ks), spec_pow(max0(vdot(h.N, H)), ob.n));
             C3 lc = {lw1.x, lw1.y, lw1.z};
             // the cumulative mask after this light: the earlier lights'
             // times this light's factors (one product, reassociated)
             const float mcum = clamp01(q.mask * prior_mask(q));
-            h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), cadd(dc, sc)));
+            h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), phong_sum(h, ob, L)));
             q.back = __float_as_int(mcum);
             h.meta += 1u << 9;                       // next light
             // stored at once, in the block that computed it: kept in registers
@@ -1291,7 +1296,29 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
                 // shading code)
                 int next = light + 1;
                 asm volatile("" : "+v"(next));
+                // The node's last light, with a Phong sum of exactly 0: its
+                // term lc * mask * 0 is 0 whatever the ray meets, and its mask
+                // is not used after the light loop (main.cpp:788 starts the
+                // next node's at 1).  A prior mask of 0 makes the query a known
+                // one (counted, not searched) and its term 0 (Params::
+                // last_light_skip: finite light colours, no NaN factor).
+                // Tested before the query is set up, while the node's N, I
+                // and colour are still in registers.
+                bool zero = false;
+#ifndef RT_LLSKIP
+#define RT_LLSKIP 1
+#endif
+                if (RT_LLSKIP && p.last_light_skip && next == p.nl - 1) {
+                    const LightW nw = light_words(p, next);
+                    V3 Ln, sd;
+                    float dl;
+                    bool unb;
+                    light_vectors(nw, q.o, Ln, sd, dl, unb);   // Ln: the light step's L for either kind
+                    const C3 t = phong_sum(h, ob, Ln);
+                    zero = (t.r == 0.0f) & (t.g == 0.0f) & (t.b == 0.0f);
+                }
                 shadow_query(q, p, next, h.obj);
+                if (zero) q.back = __float_as_int(0.0f);
                 ls.top = top;
                 return RK_SHADOW;
             }

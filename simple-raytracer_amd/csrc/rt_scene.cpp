@@ -76,6 +76,7 @@ struct rt_scene {
     long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
     long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
     long long opt_count_tests = kCountTests;   // 1: count executed ray-box / face / sphere tests
+    int last_light_skip_auto = 0;      // Params::last_light_skip when exact for the scene
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
     float4 *d_leafrec = nullptr;
@@ -512,6 +513,13 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.depth = desc->depth;
     p.dir_bf = 0;                      // set with the BVH (build_bvh); the scan needs none
     p.shadow_early_out = in.nan_fac ? 0 : 1;
+    // the last light's zero-Phong skip is exact when no factor is NaN (the
+    // masks stay in [0, 1]) and every light colour is finite (lc * 0 = 0)
+    bool lc_finite = true;
+    for (const LightK &l : in.lights)
+        for (float c : l.col) lc_finite = lc_finite && std::isfinite(c);
+    s->last_light_skip_auto = p.shadow_early_out && lc_finite ? 1 : 0;
+    p.last_light_skip = s->last_light_skip_auto;
     p.chunk = 0;                       // launch_one: chunk_for, refill_for
     p.refill_min = 1;
     p.gate_x = kGateX;
@@ -589,6 +597,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         else if (k == "bvh_threads") s->opt_bvh_threads = std::max(0LL, std::min(256LL, value));
         else s->opt_bvh_node = std::max(0LL, value);
         s->bvh_D = -1.0;               // rebuild on the next render
+    }
+    else if (k == "last_light_skip") {       // -1 auto (exact scenes), 0 off; never on where inexact
+        if (value < -1 || value > 0) return RT_E_INVALID;
+        s->base.last_light_skip = value < 0 ? s->last_light_skip_auto : 0;
     }
     else if (k == "count_tests") {
         if (value < 0 || value > 1) return RT_E_INVALID;
