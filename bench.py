@@ -77,6 +77,10 @@ def parse_args():
                     help="N>1: what rank 0 gathers -- f32 rows (12 B per pixel) or the P3 writer's "
                          "pixel values as bytes (3 B, quantised on each rank's GPU; exact for values "
                          "0..255). auto = u8 unless the warm-up frame has a value outside 0..255")
+    ap.add_argument("--count-render", default="on", choices=["on", "off"],
+                    help="after the timed region, one more render by the kernel instantiation that "
+                         "counts executed ray-box / face / sphere tests (the roofline's FLOPs); off for "
+                         "PMC passes that divide a run's counters by its renders")
     ap.add_argument("--out-json", default=None)
     return ap.parse_args()
 
@@ -257,7 +261,7 @@ def main() -> None:
             f = ff
         return bool(int(f.item()))
 
-    for k in range(max(1, args.warmup)):
+    for k in range(args.warmup if fmt == "f32" else max(1, args.warmup)):
         step(k)
     torch.cuda.synchronize()
     if fmt == "u8" and any_flag():
@@ -321,8 +325,10 @@ def main() -> None:
     # timed frames run without them); the roofline divides them by the
     # uncounted launch's time above
     try:
+        if args.count_render == "off":
+            raise rtamd.RTError("no counting render")
         gs.set_option("count_tests", 1)
-    except rtamd.RTError:         # a library before the option (A/B baselines): it always counts
+    except rtamd.RTError:         # off, or a library before the option (A/B baselines: it always counts)
         st_tests = st
     else:
         step(0)

@@ -41,7 +41,7 @@ i=0
 while read -r pass; do
   [ -z "$pass" ] && continue
   i=$((i+1))
-  step pmc_$i timeout -k 10 300 rocprofv3 --kernel-trace --pmc $pass -d $O/pmc/p$i -o run --output-format csv -- python3 $R/bench.py --cpu-baseline off --steps 1 --warmup 0 --inflight 1
+  step pmc_$i timeout -k 10 300 rocprofv3 --kernel-trace --pmc $pass -d $O/pmc/p$i -o run --output-format csv -- python3 $R/bench.py --cpu-baseline off --steps 1 --warmup 0 --inflight 1 --count-render off
 done <<PASSES
 FETCH_SIZE
 WRITE_SIZE
@@ -56,7 +56,7 @@ cd /tmp
 for c in C4 C5; do
   for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum"; do
     n=$(echo $ctr | cut -d' ' -f1)
-    step pmc_${c}_$n timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $O/pmc_$c/p_$n -o run --output-format csv -- python3 $R/bench.py --config $c --cpu-baseline off --steps 1 --warmup 0 --inflight 1
+    step pmc_${c}_$n timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr -d $O/pmc_$c/p_$n -o run --output-format csv -- python3 $R/bench.py --config $c --cpu-baseline off --steps 1 --warmup 0 --inflight 1 --count-render off
   done
 done
 cd $R
