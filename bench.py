@@ -78,9 +78,10 @@ def parse_args():
                          "pixel values as bytes (3 B, quantised on each rank's GPU; exact for values "
                          "0..255). auto = u8 unless the warm-up frame has a value outside 0..255")
     ap.add_argument("--count-render", default="on", choices=["on", "off"],
-                    help="after the timed region, one more render by the kernel instantiation that "
-                         "counts executed ray-box / face / sphere tests (the roofline's FLOPs); off for "
-                         "PMC passes that divide a run's counters by its renders")
+                    help="after the timed region, one more render by the kernel instantiation with "
+                         "counters (rays by kind for value, executed tests for the roofline; the timed "
+                         "frames run without them); off for PMC passes that divide a run's counters by "
+                         "its renders (the line's value is then 0)")
     ap.add_argument("--out-json", default=None)
     return ap.parse_args()
 
@@ -230,6 +231,16 @@ def main() -> None:
     reserve = args.reserve if args.reserve >= 0 else (0 if world == 1 else 8)
     if reserve:
         gs.set_option("reserve", reserve)
+    # the timed frames run the kernel instantiation without counters (rays by
+    # kind, events, executed tests: registers live across the whole loop,
+    # ~4 %); one render with them after the timed region gives the counts,
+    # identical every frame (option counters; an --option counters=1 keeps them)
+    counting = not any(kv.startswith("counters=") for kv in args.option)
+    if counting:
+        try:
+            gs.set_option("counters", 0)
+        except rtamd.RTError:     # a library before the option (A/B baselines): it always counts
+            counting = False
     if F > 1:
         gs.set_option("inflight", F)
     gs.prepare(cam, W, H)                 # BVH + every slot's frame buffer, before any step
@@ -312,29 +323,25 @@ def main() -> None:
     step(0)
     torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - lat0) * 1e3
-    st = gs.last_stats()          # counters of that render (identical every step)
+    st_time = gs.last_stats()     # that render's clock
     dbg = gs.debug_counters()
-    my_rays = st.rays()
     # device time of one launch with no other frame on the CUs (first wave start
     # .. last wave end on the kernel's own clock; what rocprofv3 reports per
     # dispatch at --inflight 1)
-    kernel_ms = [st.kernel_ms]
-    # the executed ray-box / face / sphere tests come from one more render by
-    # the counting instantiation of the kernel (option count_tests: its
-    # counters, live across the whole loop, cost the traversal ~1 %, so the
-    # timed frames run without them); the roofline divides them by the
-    # uncounted launch's time above
-    try:
-        if args.count_render == "off":
-            raise rtamd.RTError("no counting render")
-        gs.set_option("count_tests", 1)
-    except rtamd.RTError:         # off, or a library before the option (A/B baselines: it always counts)
-        st_tests = st
-    else:
+    kernel_ms = [st_time.kernel_ms]
+    # the counts (rays by kind for `value`, known-zero shadow rays, executed
+    # tests for the roofline) from one more render by the counting
+    # instantiation; the roofline divides its tests by the uncounted launch's
+    # time above
+    st = st_time
+    if counting and args.count_render == "on":
+        gs.set_option("counters", 1)
         step(0)
         torch.cuda.synchronize()
-        st_tests = gs.last_stats()
-        gs.set_option("count_tests", 0)
+        st = gs.last_stats()
+        gs.set_option("counters", 0)
+    st_tests = st
+    my_rays = st.rays()
 
     t = torch.tensor([elapsed, float(my_rays), float(np.mean(kernel_ms)), latency_ms], dtype=torch.float64,
                      device="cuda" if args.dist_backend == "nccl" else "cpu")

@@ -176,7 +176,7 @@ static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack -
 #define RT_BLOCK 256                     // lanes per workgroup of render_kernel
 #endif
 constexpr int kBlock = RT_BLOCK;
-constexpr long long kCountTests = 0;     // option count_tests default (the counting kernel is slower)
+constexpr long long kCounters = 1;       // option counters default (the instantiation without is ~4 % faster)
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /
@@ -235,9 +235,9 @@ int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes);
 size_t cold_frame_bytes(int maxf);
 // rt_quantize_u8 (rgb: n floats, 16-B aligned; out: n bytes, 4-B aligned)
 hipError_t quantize_u8_launch(const float *rgb, size_t n, unsigned char *out, unsigned *flag, hipStream_t st);
-// tests: the instantiation that counts executed ray-box / face / sphere tests
-// (option count_tests; rt_kernels.hip RT_COUNT)
-hipError_t render_launch(int maxf, int mode, bool tests, const Params &p, unsigned grid, size_t lds_bytes,
+// count: the instantiation with the counters (rays by kind, events, executed
+// tests; option counters; rt_kernels.hip RT_COUNT)
+hipError_t render_launch(int maxf, int mode, bool count, const Params &p, unsigned grid, size_t lds_bytes,
                          hipStream_t st);
 hipError_t deinterleave_launch(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
                                hipStream_t st);

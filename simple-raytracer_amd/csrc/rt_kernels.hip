@@ -33,17 +33,19 @@
 
 namespace rt {
 
-// Executed-test counters (rt_stats box / face / sphere tests): only in the
-// counting instantiation of the kernel (render_kernel<.., TESTS = true>,
-// option count_tests); in the other one they are compiled out -- their
-// registers, live across the whole loop, cost the traversal.
-// RT_COUNT(x) runs x where a counter object `cnt` of a counting type is in
-// scope; RT_COUNT_IF(on, x) where the switch is a template parameter.
+// Counters (rt_stats: rays by kind, known-zero shadow rays, brute-force
+// queries, SKIP_TRANS and ub_back events, executed ray-box / face / sphere
+// tests): only in the counting instantiation of the kernel
+// (render_kernel<.., COUNT = true>, option counters, the default); in the
+// other one they are compiled out -- their registers, live across the whole
+// loop, cost the traversal ~4 %.  RT_COUNT(x) runs x where a
+// counter object `cnt` of a counting type is in scope; RT_COUNT_IF(on, x)
+// where the switch is a template parameter.
 #define RT_COUNT_IF(on, x) \
     do {                   \
         if constexpr (on) { x; } \
     } while (0)
-#define RT_COUNT(x) RT_COUNT_IF(std::remove_reference_t<decltype(cnt)>::kTests, x)
+#define RT_COUNT(x) RT_COUNT_IF(std::remove_reference_t<decltype(cnt)>::kCount, x)
 
 // Read-only scene data seen through the constant address space: the loads
 // are wave-uniform and invariant, so they become scalar (s_load) reads into
@@ -166,12 +168,12 @@ __device__ __forceinline__ bool sphere_test(float4 s, V3 o, V3 d, float &t1, flo
 
 // The scan every active lane of the wave runs together.  SRC_LDS: primitive
 // arrays were staged into LDS (lds_f, lds_s); otherwise scalar loads.
-template <bool SRC_LDS, bool TESTS>
+template <bool SRC_LDS, bool COUNT>
 __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *lds_f, const float4 *lds_s,
                                      bool part, unsigned &ft, unsigned &st) {
     if (!part) return;
-    RT_COUNT_IF(TESTS, ft += (unsigned)p.nf);
-    RT_COUNT_IF(TESTS, st += (unsigned)p.ns);
+    RT_COUNT_IF(COUNT, ft += (unsigned)p.nf);
+    RT_COUNT_IF(COUNT, st += (unsigned)p.ns);
     for (int i = 0; i < p.nf; i++) {
         float4 f0, f1, f2, f3, f4;
         if (SRC_LDS) {
@@ -222,9 +224,9 @@ __device__ __forceinline__ void scan(Query &q, const Params &p, const float4 *ld
 // Per-lane counters kept small (VGPR pressure): ray kinds are counted per
 // wave with ballots in the main loop (scalar registers); only the rare events
 // and the executed-test counts stay per lane.
-template <bool TESTS>
+template <bool COUNT>
 struct CountersT {
-    static constexpr bool kTests = TESTS;
+    static constexpr bool kCount = COUNT;
     unsigned skip, ub;
     unsigned boxes, ftests, stests;             // ray-box, ray-face, ray-sphere tests executed
 #if RT_PROF
@@ -1109,7 +1111,7 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
                 n--;
             } else {
                 m.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
-                cnt.ub++;
+                RT_COUNT(cnt.ub++);
                 ub_note(p, pix);
             }
             m.et = n > 0 ? row(p.objs, c.stack[n - 1]).eta : p.eta_bkg;
@@ -1324,7 +1326,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             }
         } else if (phase == PH_REFR) {
             if (q.skipped) {
-                cnt.skip++;                          // tmp_transparency stays 0
+                RT_COUNT(cnt.skip++);                // tmp_transparency stays 0
                 set_phase(h, PH_REFL);
             } else if (q.win >= 0) {
                 m = refr_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0, cnt, pix);
@@ -1484,7 +1486,7 @@ __device__ __forceinline__ V3 primary_dir(const Params &p, int x, int y) {
     return vnorm(vsub(pt, V3{p.eye[0], p.eye[1], p.eye[2]}));
 }
 
-template <int MAXF, int MODE, bool TESTS>
+template <int MAXF, int MODE, bool COUNT>
 __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) {
     constexpr bool SRC_LDS = MODE == MODE_SCAN_LDS;
     // LDS: every lane's shading state (kLdsHot words, kBlock apart), then the
@@ -1507,7 +1509,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     LaneState<MAXF> ls;
     ls.top = -1;
     ls.frames = p.frames;
-    CountersT<TESTS> cnt = {0, 0, 0, 0, 0};
+    CountersT<COUNT> cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;
     int *stk = reinterpret_cast<int *>(lds) + threadIdx.x;  // MODE_BVH: stack[k * kBlock]
@@ -1726,11 +1728,13 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         }
         const bool search = pending && !known && !held;
 
-        w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
-        w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
-        w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
-        w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
-        w_known += (unsigned)__popcll(__ballot(known));
+        if constexpr (COUNT) {
+            w_prim += (unsigned long long)__popcll(__ballot(kind == RK_PRIMARY));
+            w_shadow += (unsigned long long)__popcll(__ballot(kind == RK_SHADOW));
+            w_refr += (unsigned long long)__popcll(__ballot(kind == RK_REFR));
+            w_refl += (unsigned long long)__popcll(__ballot(kind == RK_REFL));
+            w_known += (unsigned)__popcll(__ballot(known));
+        }
         if (MODE == MODE_BVH) {
             // dir_bf == 1: directional shadow rays go to the scan (a light's
             // shadow-region tree could not be built)
@@ -1790,35 +1794,33 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #endif
             bool need = search && q.bf;
             const unsigned long long nb = __ballot(need);
-            w_bf += (unsigned)__popcll(nb);
-            if (nb) scan<false, TESTS>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
+            if constexpr (COUNT) w_bf += (unsigned)__popcll(nb);
+            if (nb) scan<false, COUNT>(q, p, lds_f, lds_s, need, cnt.ftests, cnt.stests);
 #if RT_PROF
             pc_bf += __builtin_amdgcn_s_memtime() - c2;
 #endif
         } else {
-            scan<SRC_LDS, TESTS>(q, p, lds_f, lds_s, search, cnt.ftests, cnt.stests);
+            scan<SRC_LDS, COUNT>(q, p, lds_f, lds_s, search, cnt.ftests, cnt.stests);
         }
     }
     unsigned long long *st = p.stats;
     // this workgroup's copy of the exit counters (rt_device.h kStatCopies)
     unsigned long long *sc = st + stat_copy_off((int)(blockIdx.x & (kStatCopies - 1)));
-#ifndef RT_AB_NOSTATS                        // (A/B probe only: no exit counters but the clock)
-    if (lane == 0) {
-        atomicAdd(&sc[0], w_prim);
-        atomicAdd(&sc[1], w_shadow);
-        atomicAdd(&sc[2], w_refr);
-        atomicAdd(&sc[3], w_refl);
-        atomicAdd(&sc[32], (unsigned long long)w_known);
-        atomicAdd(&sc[33], (unsigned long long)w_bf);
-    }
-    atomicAdd(&sc[4], (unsigned long long)cnt.skip);
-    atomicAdd(&sc[5], (unsigned long long)cnt.ub);
-    if constexpr (TESTS) {
+    if constexpr (COUNT) {
+        if (lane == 0) {
+            atomicAdd(&sc[0], w_prim);
+            atomicAdd(&sc[1], w_shadow);
+            atomicAdd(&sc[2], w_refr);
+            atomicAdd(&sc[3], w_refl);
+            atomicAdd(&sc[32], (unsigned long long)w_known);
+            atomicAdd(&sc[33], (unsigned long long)w_bf);
+        }
+        atomicAdd(&sc[4], (unsigned long long)cnt.skip);
+        atomicAdd(&sc[5], (unsigned long long)cnt.ub);
         atomicAdd(&sc[6], (unsigned long long)cnt.boxes);
         atomicAdd(&sc[7], (unsigned long long)cnt.ftests);
         atomicAdd(&sc[8], (unsigned long long)cnt.stests);
     }
-#endif
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
         atomicMax(&sc[24], ~t_start);                // kernel start (first wave): the counters start
@@ -1956,28 +1958,28 @@ int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes) {
     return blocks_mode<17>(mode, lds_bytes);
 }
 
-template <int MAXF, bool TESTS>
+template <int MAXF, bool COUNT>
 static hipError_t launch_mode(int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st) {
     if (mode == MODE_BVH)
-        hipLaunchKernelGGL((render_kernel<MAXF, MODE_BVH, TESTS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
+        hipLaunchKernelGGL((render_kernel<MAXF, MODE_BVH, COUNT>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
     else if (mode == MODE_SCAN_LDS)
-        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN_LDS, TESTS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
+        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN_LDS, COUNT>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
     else
-        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN, TESTS>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
+        hipLaunchKernelGGL((render_kernel<MAXF, MODE_SCAN, COUNT>), dim3(grid), dim3(kBlock), lds_bytes, st, p);
     return hipGetLastError();
 }
 
-template <bool TESTS>
+template <bool COUNT>
 static hipError_t launch_maxf(int maxf, int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st) {
-    if (maxf == 5) return launch_mode<5, TESTS>(mode, p, grid, lds_bytes, st);
-    if (maxf == 9) return launch_mode<9, TESTS>(mode, p, grid, lds_bytes, st);
-    if (maxf == 17) return launch_mode<17, TESTS>(mode, p, grid, lds_bytes, st);
+    if (maxf == 5) return launch_mode<5, COUNT>(mode, p, grid, lds_bytes, st);
+    if (maxf == 9) return launch_mode<9, COUNT>(mode, p, grid, lds_bytes, st);
+    if (maxf == 17) return launch_mode<17, COUNT>(mode, p, grid, lds_bytes, st);
     return hipErrorInvalidValue;
 }
 
-hipError_t render_launch(int maxf, int mode, bool tests, const Params &p, unsigned grid, size_t lds_bytes,
+hipError_t render_launch(int maxf, int mode, bool count, const Params &p, unsigned grid, size_t lds_bytes,
                          hipStream_t st) {
-    return tests ? launch_maxf<true>(maxf, mode, p, grid, lds_bytes, st)
+    return count ? launch_maxf<true>(maxf, mode, p, grid, lds_bytes, st)
                  : launch_maxf<false>(maxf, mode, p, grid, lds_bytes, st);
 }
 

@@ -75,7 +75,7 @@ struct rt_scene {
     AccelInput in;                     // host arrays + BVH sources (rt_accel.h)
     long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
     long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
-    long long opt_count_tests = kCountTests;   // 1: count executed ray-box / face / sphere tests
+    long long opt_counters = kCounters;  // 1: the counting kernel (rt_stats' rays, events, tests); 0: none
     int last_light_skip_auto = 0;      // Params::last_light_skip when exact for the scene
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
@@ -201,7 +201,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     s->last_lights_in_lds = pl.lights_in_lds;
     s->last_work_parts = 1 << pl.work_shift;
     if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
-    return render_launch(maxf, mode, s->opt_count_tests != 0, pl, (unsigned)grid, shm, st);
+    return render_launch(maxf, mode, s->opt_counters != 0, pl, (unsigned)grid, shm, st);
 }
 
 // (Re)build the BVH for distance bound D on the host (rt_accel.cpp) and
@@ -602,9 +602,9 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         if (value < -1 || value > 0) return RT_E_INVALID;
         s->base.last_light_skip = value < 0 ? s->last_light_skip_auto : 0;
     }
-    else if (k == "count_tests") {
+    else if (k == "counters") {
         if (value < 0 || value > 1) return RT_E_INVALID;
-        s->opt_count_tests = value;
+        s->opt_counters = value;
     }
     else if (k == "hot_copies") {
         if (value < 0 || value > 64 || (value & (value - 1))) return RT_E_INVALID;
@@ -797,7 +797,7 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[43] = (unsigned long long)s->last_lights_in_lds;
     h[45] = (unsigned long long)s->last_work_parts;
     h[44] = (unsigned long long)s->last_hot_copies;
-    h[48] = (unsigned long long)s->opt_count_tests;
+    h[48] = (unsigned long long)s->opt_counters;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;
 }

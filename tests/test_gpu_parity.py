@@ -63,7 +63,7 @@ def test_scene_parity_forced_path(name, accel, golden):
     """Both search strategies on every small fixture: the brute-force scan
     (accel=0) and the BVH (accel=1, with its exact fallbacks), each against
     the oracle, with identical ray counts."""
-    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel, "count_tests": 1})
+    img, st = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel})
     ref, cnt = OracleScene(name, cwd=SCENES).render()
     c = compare(img, ref)
     tag = "accel%d" % accel
@@ -726,19 +726,19 @@ def test_refill_options_bit_identical():
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
 
-def test_work_bands_hot_copies_count_tests_bit_identical():
+def test_work_bands_hot_copies_counters_bit_identical():
     """Option work_parts (bands of the work items with a pixel counter each,
     auto = one per XCD), option hot_copies (copies of the BVH's top 64
     nodes and their leaves; each wave starts its searches in one) and option
-    count_tests (the kernel instantiation that counts executed ray-box / face
-    / sphere tests) change which lane renders which pixel and where a search
+    counters (0: the kernel instantiation without the counters, which the
+    bench times) change which lane renders which pixel and where a search
     reads the tree's top, never a pixel: the image and ray counts equal the default render's bit
     for bit, which equals the oracle's.  C2 has fewer nodes than one copy
     holds (the whole tree is copied), C5 at depth 8 has 37 864."""
     variants = [{"work_parts": w} for w in (1, 2, 4, 8)]
     variants += [{"hot_copies": k} for k in (0, 2, 16, 64)] + [{"hot_copies": 16, "work_parts": 1, "chunk": 100}]
-    # the counting instantiation (option count_tests) renders the same
-    variants += [{"count_tests": 1}, {"count_tests": 1, "work_parts": 1}]
+    # the instantiation without counters renders the same image (its counts are 0)
+    variants += [{"counters": 0}, {"counters": 0, "work_parts": 1}, {"counters": 0, "hot_copies": 16}]
     for name, depth in (("C2_128x128.txt", None), ("C3_64x64.txt", None), ("C5_8x8.txt", 8)):
         ref, st = rtamd.render_scene(name, cwd=SCENES, depth=depth)
         o = OracleScene(name, cwd=SCENES)
@@ -750,21 +750,23 @@ def test_work_bands_hot_copies_count_tests_bit_identical():
         for opts in variants:
             img, st2 = rtamd.render_scene(name, cwd=SCENES, depth=depth, options=opts)
             assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, opts)
-            assert _counts(st2) == _counts(st), (name, opts)
+            if opts.get("counters", 1):
+                assert _counts(st2) == _counts(st), (name, opts)
+            else:
+                assert st2.rays() == 0 and st2.box_tests == 0 and st2.kernel_ms > 0, (name, opts)
     hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
     gs = rtamd.GpuScene(hs)
     gs.set_option("hot_copies", 16)
     gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
     dbg = gs.debug_counters()
-    assert dbg[44] == 16 and dbg[48] == 0 and dbg[45] == 8
-    st0 = gs.last_stats()
-    assert st0.box_tests == 0 and st0.sphere_tests == 0      # not counted by default
-    gs.set_option("count_tests", 1)
-    gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
+    assert dbg[44] == 16 and dbg[48] == 1 and dbg[45] == 8          # counted by default
     st1 = gs.last_stats()
-    assert gs.debug_counters()[48] == 1 and st1.box_tests > 0 and st1.sphere_tests > 0 and st1.face_tests > 0
-    assert _counts(st1) == _counts(st0)
-    for bad in ({"hot_copies": 3}, {"hot_copies": 128}, {"work_parts": 3}, {"count_tests": 2}):
+    assert st1.box_tests > 0 and st1.sphere_tests > 0 and st1.face_tests > 0 and st1.rays() > 0
+    gs.set_option("counters", 0)
+    gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
+    st0 = gs.last_stats()
+    assert gs.debug_counters()[48] == 0 and st0.rays() == 0 and st0.box_tests == 0
+    for bad in ({"hot_copies": 3}, {"hot_copies": 128}, {"work_parts": 3}, {"counters": 2}):
         with pytest.raises(rtamd.RTError):
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
@@ -843,7 +845,7 @@ def test_bvh_collapse_parity(opts):
     oracle and identical ray counts on C3 (2000 objects) and C5 (100 000
     spheres, depth 8), for the greedy collapse and another node cost."""
     for name, depth in (("C3_64x64.txt", 4), ("C5_8x8.txt", 8)):
-        img, st = rtamd.render_scene(name, cwd=SCENES, depth=depth, options={**opts, "count_tests": 1})
+        img, st = rtamd.render_scene(name, cwd=SCENES, depth=depth, options=opts)
         o = OracleScene(name, cwd=SCENES)
         o.set_depth(depth)
         ref, cnt = o.render()

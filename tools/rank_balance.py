@@ -53,6 +53,14 @@ def main():
     pipe = rtamd.GpuScene(hs)                  # bench.py's N > 1 setting
     pipe.set_option("inflight", a.inflight)
     pipe.set_option("reserve", a.reserve)
+    # timed renders run the kernel without counters, as bench.py's timed
+    # frames do; one counted render per rank gives its rays
+    counted = rtamd.GpuScene(hs)
+    for g in (alone, pipe):
+        try:
+            g.set_option("counters", 0)
+        except rtamd.RTError:                  # a library before the option: it always counts
+            pass
     for kv in a.option:
         k, v = kv.split("=")
         alone.set_option(k, int(v))
@@ -101,11 +109,13 @@ def main():
         ranks = []
         for r in range(n):
             y0, b, step, nr, per = row_set(H, n, r)
+            counted.render_row_blocks_async(cam, W, H, y0, b, step, nr, bufs[0].data_ptr())
+            rays = counted.last_stats().rays()
             for _ in range(2):
                 alone.render_row_blocks_async(cam, W, H, y0, b, step, nr, bufs[0].data_ptr())
                 st = alone.last_stats()
             ms_pipe = pipelined(y0, b, step, nr, a.frames)
-            ranks.append(dict(rank=r, rows=nr, rays=st.rays(), kernel_ms=round(st.kernel_ms, 3),
+            ranks.append(dict(rank=r, rows=nr, rays=rays, kernel_ms=round(st.kernel_ms, 3),
                               pipelined_ms=round(ms_pipe, 3)))
             print(n, ranks[-1], flush=True)
         rays = sum(x["rays"] for x in ranks)
