@@ -1,5 +1,6 @@
 #!/bin/bash
-# End-of-round evidence on one GPU box (all outputs under gpurun_out/final/):
+# End-of-round evidence on one GPU box (all outputs under gpurun_out/final/;
+# round 4: copied to profiles/r04/final_*):
 # smoke, the GPU test suite, one bench line per config, a rocprofv3 kernel
 # trace of the default bench at one frame in flight and at two, the PMC
 # passes whose FETCH_SIZE / WRITE_SIZE give profiles/pmc_traffic.json
@@ -26,9 +27,10 @@ for c in C4 C5; do
   step bench_$c bash -c "timeout -k 10 600 python bench.py --config $c --cpu-baseline off --steps 8 --warmup 2 > $O/${c}_bench.json 2> $O/${c}_bench.err"
 done
 step e2e bash -c "timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 > $O/e2e.txt 2>&1"
-for c in C3 C4 C5; do
+for c in C3 C4; do
   step bal_$c bash -c "timeout -k 10 600 python -u tools/rank_balance.py $c --ns 1,2,4,8 > $O/${c}_row_balance.txt 2>&1"
 done
+step bal_C5 bash -c "timeout -k 10 600 python -u tools/rank_balance.py C5 --ns 1,8 --frames 8 > $O/C5_row_balance.txt 2>&1"
 fi
 if [ "$PART" = all ] || [ "$PART" = b ]; then
 cd /tmp
@@ -62,5 +64,9 @@ done
 cd $R
 for c in C4 C5; do RENDERS=2 python3 tools/pmc_summary.py $O/pmc_$c > $O/${c}_pmc.json; done
 step timeline bash -c "RTAMD_LIB_DIR=$R/simple-raytracer_amd/lib_prof timeout -k 10 200 python -u tools/timeline.py C2 > $O/tl_C2.txt 2>&1"
+step timeline_C3r8 bash -c "RTAMD_LIB_DIR=$R/simple-raytracer_amd/lib_prof timeout -k 10 200 python -u tools/timeline.py C3 --rows 8:0 > $O/tl_C3_r8.txt 2>&1"
+step phases_C3 bash -c "RTAMD_LIB_DIR=$R/simple-raytracer_amd/lib_prof timeout -k 10 200 python -u tools/prof_phases.py C3 > $O/phases_C3.txt 2>&1"
+step phases_C3_nc bash -c "RTAMD_LIB_DIR=$R/simple-raytracer_amd/lib_prof timeout -k 10 200 python -u tools/prof_phases.py C3 counters=0 > $O/phases_C3_nocount.txt 2>&1"
+step phases_C5 bash -c "RTAMD_LIB_DIR=$R/simple-raytracer_amd/lib_prof timeout -k 10 300 python -u tools/prof_phases.py C5 > $O/phases_C5.txt 2>&1"
 fi
 echo done
