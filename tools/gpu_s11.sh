@@ -19,3 +19,7 @@ for v in lib lib_nt; do
 done
 cd $R
 for v in lib lib_nt; do RTAMD_LIB_DIR=$R/simple-raytracer_amd/$v RENDERS=2 python3 tools/pmc_summary.py $O/pmc_C5_$v > $O/C5_pmc_$v.json; done
+# the N=8 C3 share, pipelined: frames in flight and reserved slots
+for f in 4 8; do for r in 0 8; do
+  timeout -k 10 120 python -u tools/rank_balance.py C3 --ns 1,8 --rank-only 0 --inflight $f --reserve $r > $O/rb8_C3_f${f}_r${r}.txt 2>&1
+done; done

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--reserve", type=int, default=8)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--option", action="append", default=[], help="kernel option key=value (both scenes)")
+    ap.add_argument("--rank-only", type=int, default=-1, help="measure only this rank of each N (a sweep)")
     a = ap.parse_args()
 
     import torch
@@ -107,7 +108,7 @@ def main():
     base = None
     for n in (int(v) for v in a.ns.split(",")):
         ranks = []
-        for r in range(n):
+        for r in (range(n) if a.rank_only < 0 else [min(a.rank_only, n - 1)]):
             y0, b, step, nr, per = row_set(H, n, r)
             counted.render_row_blocks_async(cam, W, H, y0, b, step, nr, bufs[0].data_ptr())
             rays = counted.last_stats().rays()
@@ -118,7 +119,7 @@ def main():
             ranks.append(dict(rank=r, rows=nr, rays=rays, kernel_ms=round(st.kernel_ms, 3),
                               pipelined_ms=round(ms_pipe, 3)))
             print(n, ranks[-1], flush=True)
-        rays = sum(x["rays"] for x in ranks)
+        rays = sum(x["rays"] for x in ranks) * (n if a.rank_only >= 0 else 1)   # (one rank: x n)
         k = [x["kernel_ms"] for x in ranks]
         p = [x["pipelined_ms"] for x in ranks]
         strip_bytes = row_set(H, n, 0)[4] * W * 3 * bpp
