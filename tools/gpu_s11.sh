@@ -23,3 +23,6 @@ for v in lib lib_nt; do RTAMD_LIB_DIR=$R/simple-raytracer_amd/$v RENDERS=2 pytho
 for f in 4 8; do for r in 0 8; do
   timeout -k 10 120 python -u tools/rank_balance.py C3 --ns 1,8 --rank-only 0 --inflight $f --reserve $r > $O/rb8_C3_f${f}_r${r}.txt 2>&1
 done; done
+for q in 8 16; do
+  GPU_MAX_HW_QUEUES=$q timeout -k 10 120 python -u tools/rank_balance.py C3 --ns 1,8 --rank-only 0 --inflight 8 --reserve 8 > $O/rb8_C3_q$q.txt 2>&1
+done
