@@ -228,6 +228,9 @@ constexpr int kLdsHotWords = 16;         // per-lane shading state words in LDS 
 // MAXF, the ShadeRay frames per lane an instantiation holds, for a recursion
 // depth: 5 (depth <= 4), 9 (<= 8), 17 (<= 16); -1 above
 int maxf_for_depth(int depth);
+// the instantiation for a scene: 1 when no material reflects or refracts (or
+// depth 0), else by depth (-1: deeper than supported)
+int maxf_for(int depth, bool secondary);
 // resident workgroups per CU of render_kernel<maxf, mode> with `lds_bytes` of
 // dynamic LDS (0 if it cannot launch)
 int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes);

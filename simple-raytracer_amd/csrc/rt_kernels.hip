@@ -1242,6 +1242,15 @@ __device__ __forceinline__ void closest_query(Query &q, const Params &p, V3 d, i
     q.win = -1;
 }
 
+// MAXF = 1: the instantiation for scenes where no material reflects or
+// refracts (or depth 0): the recursion's code is compiled out -- its
+// conditions are false at run time there anyway (launch: maxf_for) -- and
+// the registers it frees carry the last light's zero-Phong skip, which costs
+// the recursive instantiations more than it saves them (C3 -2.1 %, C5 -1.8 %;
+// C4 +2.6 %, profiles/r04/ab/llskip_*.txt).
+template <int MAXF>
+constexpr bool kRecurse = MAXF > 1;
+
 // A light's diffuse + specular sum for light direction L (main.cpp:930-950)
 __device__ __forceinline__ C3 phong_sum(const HotR &h, const ObjK &ob, V3 L) {
     // H only feeds the specular power: rsqrt instead of 3 IEEE divisions
@@ -1321,7 +1330,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
 #ifndef RT_LLSKIP
 #define RT_LLSKIP 1
 #endif
-                if (RT_LLSKIP && p.last_light_skip && next == p.nl - 1) {
+                if (RT_LLSKIP && !kRecurse<MAXF> && p.last_light_skip && next == p.nl - 1) {
                     const LightW nw = light_words(p, next);
                     V3 Ln, sd;
                     float dl;
@@ -1389,7 +1398,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             // refract: the reference computes them for every node
             // (main.cpp:961-992), but they feed nothing else, and a wave with
             // no such lane then skips the asinf / acosf / double Schlick code
-            bool refr = p.depth - top > 0 && (double)ob.opacity < 1.0 && ob.eta > 0;
+            bool refr = kRecurse<MAXF> && p.depth - top > 0 && (double)ob.opacity < 1.0 && ob.eta > 0;
             float cosI = 0.0f, snell = 0.0f;
             if (refr) {
                 cosI = cos_i(h);
@@ -1419,7 +1428,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             const ObjK &ob = row(p.objs, h.obj);
             const float cosI = cos_i(h);
             float Fr = refl_fresnel(ob, cosI);
-            if (p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
+            if (kRecurse<MAXF> && p.depth - top > 0 && (double)Fr != 0.0 && (double)ob.ks > 0.0) {
                 V3 R = vsub(vmul(h.N, (float)(2.0 * (double)cosI)), h.I);
                 closest_query(q, p, R, h.obj);
                 h.dif.r = Fr;                        // for the child's return or the miss (F_t is done with)
@@ -1943,8 +1952,10 @@ int maxf_for_depth(int depth) {
     return depth <= 4 ? 5 : depth <= 8 ? 9 : depth <= 16 ? 17 : -1;
 }
 
+int maxf_for(int depth, bool secondary) { return !secondary || depth <= 0 ? 1 : maxf_for_depth(depth); }
+
 size_t cold_frame_bytes(int maxf) {
-    return maxf == 5 ? sizeof(Cold<5>) : maxf == 9 ? sizeof(Cold<9>) : sizeof(Cold<17>);
+    return maxf == 1 ? sizeof(Cold<1>) : maxf == 5 ? sizeof(Cold<5>) : maxf == 9 ? sizeof(Cold<9>) : sizeof(Cold<17>);
 }
 
 template <int MAXF, int MODE>
@@ -1964,6 +1975,7 @@ static int blocks_mode(int mode, size_t lds_bytes) {
 }
 
 int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes) {
+    if (maxf == 1) return blocks_mode<1>(mode, lds_bytes);
     if (maxf == 5) return blocks_mode<5>(mode, lds_bytes);
     if (maxf == 9) return blocks_mode<9>(mode, lds_bytes);
     return blocks_mode<17>(mode, lds_bytes);
@@ -1982,6 +1994,7 @@ static hipError_t launch_mode(int mode, const Params &p, unsigned grid, size_t l
 
 template <bool COUNT>
 static hipError_t launch_maxf(int maxf, int mode, const Params &p, unsigned grid, size_t lds_bytes, hipStream_t st) {
+    if (maxf == 1) return launch_mode<1, COUNT>(mode, p, grid, lds_bytes, st);
     if (maxf == 5) return launch_mode<5, COUNT>(mode, p, grid, lds_bytes, st);
     if (maxf == 9) return launch_mode<9, COUNT>(mode, p, grid, lds_bytes, st);
     if (maxf == 17) return launch_mode<17, COUNT>(mode, p, grid, lds_bytes, st);

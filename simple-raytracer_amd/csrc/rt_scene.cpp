@@ -300,7 +300,8 @@ int build_bvh(rt_scene *s, double D) {
 
 int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = false) {
     int depth = p.depth < 0 ? 0 : p.depth;
-    if (maxf_for_depth(depth) < 0) return RT_E_UNSUPPORTED;
+    const int maxf = maxf_for(depth, s->secondary);
+    if (maxf < 0) return RT_E_UNSUPPORTED;
     int nobj = p.nf + p.ns;
     bool bvh = s->opt_accel == 1 || (s->opt_accel == -1 && nobj > 32);
     int mode = MODE_SCAN;
@@ -331,7 +332,7 @@ int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = 
     // workgroup above ~31 KB of LDS loses a resident workgroup per CU in
     // practice (profiles/r02/ab_lds_stack.txt, profiles/r03/ab_deep_stack.txt)
     p.stack_cap = s->opt_lds_stack > 0 ? (int)s->opt_lds_stack : depth > 4 ? kLdsStackDeep : kLdsStackDefault;
-    hipError_t e = launch_one(s, slot, p, maxf_for_depth(depth), mode, st, dry);
+    hipError_t e = launch_one(s, slot, p, maxf, mode, st, dry);
     return e == hipSuccess ? RT_OK : RT_E_HIP;
 }
 
