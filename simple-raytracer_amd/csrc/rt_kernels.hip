@@ -47,17 +47,6 @@ namespace rt {
     } while (0)
 #define RT_COUNT(x) RT_COUNT_IF(std::remove_reference_t<decltype(cnt)>::kCount, x)
 
-// RT_NT_FRAMES (A/B): frame stores with the non-temporal hint, so that the
-// frames and stack spills streaming through L2 evict the BVH's lines less
-#ifndef RT_NT_FRAMES
-#define RT_NT_FRAMES 0
-#endif
-template <class T>
-__device__ __forceinline__ void frame_store(T *dst, T v) {
-    if constexpr (RT_NT_FRAMES) __builtin_nontemporal_store(v, dst);
-    else *dst = v;
-}
-
 // Read-only scene data seen through the constant address space: the loads
 // are wave-uniform and invariant, so they become scalar (s_load) reads into
 // SGPRs through the scalar cache instead of 64 identical per-lane loads.
@@ -546,7 +535,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         const int tag = stk[0];
         const int nb = tag == rtbvh::kEmpty ? 0 : tag - kRefill;
         int *o = ovf_lane() + nb * kSpill;
-        for (int i = 0; i < kSpill; i++) frame_store(o + i, stk[(1 + i) * kBlock]);
+        for (int i = 0; i < kSpill; i++) o[i] = stk[(1 + i) * kBlock];
         for (int i = kSpill + 1; i < sp; i++) stk[(i - kSpill) * kBlock] = stk[i * kBlock];
         sp -= kSpill;
         stk[0] = kRefill + nb + 1;
@@ -880,15 +869,15 @@ static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's fram
 
 template <int MAXF>
 __device__ __forceinline__ void cold_save_head(Cold<MAXF> &c, const HotR &h, float f) {
-    frame_store(reinterpret_cast<f4v *>(&c.head), f4v{h.acc.r, h.acc.g, h.acc.b, f});
-    frame_store(&c.meta, h.meta);
+    reinterpret_cast<f4v &>(c.head) = f4v{h.acc.r, h.acc.g, h.acc.b, f};
+    c.meta = h.meta;
 }
 template <int MAXF>
 __device__ __forceinline__ void cold_save_ext(Cold<MAXF> &c, V3 P, const HotR &h) {
     f4v *v = reinterpret_cast<f4v *>(c.ext);
-    frame_store(v + 0, f4v{h.N.x, h.N.y, h.N.z, h.I.x});
-    frame_store(v + 1, f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei});
-    frame_store(v + 2, f4v{h.et, P.x, P.y, P.z});
+    v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
+    v[1] = f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei};
+    v[2] = f4v{h.et, P.x, P.y, P.z};
 }
 // the head: h.acc, h.meta; returns f
 template <int MAXF>
