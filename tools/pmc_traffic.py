@@ -12,7 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 METHOD = ("rocprofv3 --kernel-trace --pmc, one counter group per pass (tools/final_session.sh, bench.py "
-          "--inflight 1 --steps 1 --warmup 0: 2 renders per pass, RENDERS=2); read = 2 x FETCH_SIZE x 1024 "
+          "--inflight 1 --steps 1 --warmup 0 --count-render off: 2 renders of the kernel without counters per pass, RENDERS=2); read = 2 x FETCH_SIZE x 1024 "
           "(gfx950 correction, MI355X_MICROARCH.md HBM), write = WRITE_SIZE x 1024")
 
 
