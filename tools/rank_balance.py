@@ -87,7 +87,7 @@ def main():
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) * 1e3 / frames
         run()                                  # warm
-        return run()
+        return min(run(), run())               # the better of two (another process on the box shows as one slow run)
 
     out = {"config": a.config, "imsize": [W, H], "frames": a.frames, "inflight": a.inflight,
            "reserve": a.reserve, "options": a.option, "note": "PROJECTED from one GPU: each rank's row set rendered alone; "
