@@ -164,12 +164,15 @@ Mat3D create_view_window_and_ray_trace(Vector3 view_origin, Vector3 view_directi
     rt_scene *scene = nullptr;
     rt_stats st{};
     int rc = rt_scene_create(0, &desc, &scene);
+    // the kernel without counters unless RT_HIP_SEAM_STATS asks for the counts below
+    const bool seam_stats = std::getenv("RT_HIP_SEAM_STATS") != nullptr;
+    if (rc == RT_OK) rc = rt_scene_set_option(scene, "counters", seam_stats ? 1 : 0);
     if (rc == RT_OK) rc = rt_render_rows(scene, &cam, W, H, 0, H, rgb.data(), &st);
     rt_scene_destroy(scene);
     if (rc != RT_OK) throw std::runtime_error(std::string("rt_hip render failed: ") + rt_strerror(rc));
     // RT_HIP_SEAM_STATS set: say that this seam ran, with the GPU's TraceRay
     // counts (a test asserts them against the reference's own call counts)
-    if (std::getenv("RT_HIP_SEAM_STATS"))
+    if (seam_stats)
         std::fprintf(stderr, "rt_hip seam: %dx%d rays primary %llu shadow %llu refraction %llu reflection %llu\n", W, H,
                      st.primary, st.shadow, st.refraction, st.reflection);
 

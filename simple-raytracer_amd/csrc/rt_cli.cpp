@@ -25,6 +25,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <memory>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -40,12 +41,29 @@ const int kRowBlock = 8;
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
 
+// The host image, uninitialised: every float is written by the device->host
+// copies before it is read (zero-filling C5's 3.2 GB took 0.53 s, more than
+// the copy itself)
+struct HostImage {
+    std::unique_ptr<float[]> p;
+    size_t n;
+    explicit HostImage(size_t count) : p(new float[count]), n(count) {}
+    float *data() { return p.get(); }
+    size_t size() const { return n; }
+    float *begin() { return p.get(); }
+};
+
+// The kernel instantiation with counters (rays by kind, executed tests)
+// only when the run reports them (--stats, --stats-json): ~4 % slower
+void set_counters(rt_scene *s, bool on) { (void)rt_scene_set_option(s, "counters", on ? 1 : 0); }
+bool g_counters = false;
+
 // One process, N devices: every device renders its row set (rth_row_set)
 // into HBM, one RCCL gather collects the N buffers on the first device, a
 // device-side de-interleave puts the rows in image order, one copy brings the
 // image to the host.  The seam is the reference's single render call
 // (main.cpp:607), its row loop (main.cpp:718) split across the devices.
-int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, int gpus, std::vector<float> &img,
+int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, int gpus, HostImage &img,
                 std::vector<rt_stats> &st) {
     struct Dev {
         int id = 0;
@@ -70,6 +88,7 @@ int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, i
         if (rth_row_set(H, gpus, g, kRowBlock, &v.y0, &v.step, &v.nrows, &v.rows_per)) fail("row set", -1);
         if (hipSetDevice(v.id) != hipSuccess) fail("hipSetDevice", v.id);
         int e = rt_scene_create(v.id, rth_desc(hs), &v.scene);
+        if (!e) set_counters(v.scene, g_counters);
         if (e) fail(rt_strerror(e), e);
         const size_t strip = (size_t)v.rows_per * W * 3 * sizeof(float);
         if (!rc && (hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking) != hipSuccess ||
@@ -195,7 +214,8 @@ int main(int argc, char *argv[]) {
         return 2;
     }
     t = Clock::now();
-    std::vector<float> img((size_t)W * H * 3);
+    g_counters = stats || stats_json;
+    HostImage img((size_t)W * H * 3);
     const double ph_alloc = ms_since(t);
     std::vector<rt_stats> st(gpus);
     std::vector<int> rcs(gpus, 0);
@@ -216,6 +236,7 @@ int main(int argc, char *argv[]) {
         float *dimg = nullptr;
         t = Clock::now();
         int r = rt_scene_create(device, rth_desc(hs), &s);
+        if (!r) set_counters(s, false);    // the timed render: no counters (they come from a second one)
         ph_create = ms_since(t);
         t = Clock::now();
         if (!r) r = rt_scene_prepare(s, &cam, W, H);
@@ -228,6 +249,14 @@ int main(int argc, char *argv[]) {
         if (!r && hipMemcpy(img.data(), dimg, img.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
             r = RT_E_HIP;
         ph_d2h = ms_since(t);
+        // --stats / --stats-json: the counts from one more render by the
+        // counting instantiation, outside the phases (its image is the same)
+        if (!r && g_counters) {
+            rt_stats timed = st[0];
+            set_counters(s, true);
+            r = rt_render_rows(s, &cam, W, H, 0, H, dimg, &st[0]);
+            st[0].kernel_ms = timed.kernel_ms;
+        }
         if (dimg) (void)hipFree(dimg);
         rt_scene_destroy(s);
         rcs[0] = r;
@@ -237,6 +266,7 @@ int main(int argc, char *argv[]) {
         pool.emplace_back([&, g] {
             rt_scene *s = nullptr;
             int r = rt_scene_create(device + g, rth_desc(hs), &s);
+            if (!r) set_counters(s, g_counters);
             if (!r) {
                 std::vector<int> rows;
                 for (int b = g * kRowBlock; b < H; b += gpus * kRowBlock)
