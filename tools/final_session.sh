@@ -33,6 +33,8 @@ done
 step bal_C5 bash -c "timeout -k 10 600 python -u tools/rank_balance.py C5 --ns 1,8 --frames 8 > $O/C5_row_balance.txt 2>&1"
 fi
 if [ "$PART" = all ] || [ "$PART" = c ]; then
+step tests_cli bash -c "timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread -k 'cli or seam or binding or smoke' > $O/pytest_gpu_cli.log 2>&1; rc=\$?; tail -2 $O/pytest_gpu_cli.log; exit \$rc"
+step e2e_c bash -c "timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 > $O/e2e.txt 2>&1"
 # this round's kernel against round 3's (lib_r3: tools/build_rev.sh 268f298 r3), interleaved
 step ab_r3_C3 bash -c "timeout -k 10 400 python -u tools/ab.py --rounds 3 --steps 100 --config C3 r4: r3:lib_r3 > $O/ab_r4_vs_r3_C3.txt 2>&1"
 step ab_r3_C2 bash -c "timeout -k 10 300 python -u tools/ab.py --rounds 3 --steps 300 --config C2 r4: r3:lib_r3 > $O/ab_r4_vs_r3_C2.txt 2>&1"
