@@ -40,6 +40,8 @@ step ab_r3_C3 bash -c "timeout -k 10 400 python -u tools/ab.py --rounds 3 --step
 step ab_r3_C2 bash -c "timeout -k 10 300 python -u tools/ab.py --rounds 3 --steps 300 --config C2 r4: r3:lib_r3 > $O/ab_r4_vs_r3_C2.txt 2>&1"
 step ab_r3_C4 bash -c "timeout -k 10 300 python -u tools/ab.py --rounds 2 --steps 20 --config C4 r4: r3:lib_r3 > $O/ab_r4_vs_r3_C4.txt 2>&1"
 step ab_r3_C5 bash -c "timeout -k 10 400 python -u tools/ab.py --rounds 2 --steps 3 --config C5 r4: r3:lib_r3 > $O/ab_r4_vs_r3_C5.txt 2>&1"
+# the C3 line again, now that profiles/pmc_traffic.json holds this library's PMC bytes
+step bench_C3_traffic bash -c "timeout -k 10 600 python bench.py > $O/C3_bench_traffic.json 2> $O/C3_bench_traffic.err"
 fi
 if [ "$PART" = all ] || [ "$PART" = b ]; then
 cd /tmp
