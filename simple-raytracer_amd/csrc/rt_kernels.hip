@@ -1732,10 +1732,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             const bool sec = pending && (k == RK_REFR || k == RK_REFL);
             const unsigned nsec = (unsigned)__popcll(__ballot(sec));
             const bool others = __ballot(pending && !sec) != 0ull;
-#ifndef RT_GATE_DRAINED
-#define RT_GATE_DRAINED 1              // 0: no hold once the work is drained (A/B)
-#endif
-            held = sec && others && nsec < p.gate_x && (RT_GATE_DRAINED || !drained);
+            held = sec && others && nsec < p.gate_x;
             held_kind = k;
         }
         const bool search = pending && !known && !held;
