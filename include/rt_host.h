@@ -52,6 +52,17 @@ void rth_quantize(const float *rgb, long long n, long long *out);
  * size_t of rth_quantize.  threads <= 0: all cores.  Returns 0 or -1. */
 int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads);
 
+/* The same file written in row blocks, in order (the CLI overlaps each
+ * block's device->host copy with the previous block's formatting):
+ * rth_ppm_open writes the header; rth_ppm_write_rows appends the next nrows
+ * rows (nrows * W * 3 floats); rth_ppm_close returns 0 only when all H rows
+ * were written without error.  Byte-identical to rth_write_ppm.  Each returns
+ * 0 or -1. */
+typedef struct rth_ppm_stream rth_ppm_stream;
+int rth_ppm_open(const char *path, int W, int H, int threads, rth_ppm_stream **out);
+int rth_ppm_write_rows(rth_ppm_stream *stream, const float *rgb, int nrows);
+int rth_ppm_close(rth_ppm_stream *stream);
+
 /* remove_extension(path) + ".ppm" (src/utility.h:34-41, main.cpp:614-616). */
 int rth_output_path(const char *scene_path, char *out, int outlen);
 

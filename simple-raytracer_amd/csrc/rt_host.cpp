@@ -529,6 +529,15 @@ inline long long quantize1(float c) {
 
 }  // namespace
 
+// An open P3 file being written row block by row block (rth_ppm_open)
+struct rth_ppm_stream {
+    int fd;
+    int W, H, rows;                    // rows written so far
+    size_t off;                        // file offset of the next row
+    int threads;
+    bool good;
+};
+
 extern "C" {
 
 int rth_parse_file(const char *path, rth_scene **out, char *msg, int msglen) {
@@ -616,13 +625,37 @@ void rth_quantize(const float *rgb, long long n, long long *out) {
 // (background > 1, NaN's INT_MIN, negative values as size_t) through
 // std::to_chars.
 int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads) {
+    rth_ppm_stream *st = nullptr;
+    if (rth_ppm_open(path, W, H, threads, &st) != 0) return -1;
+    const int rc = rth_ppm_write_rows(st, rgb, H);
+    return (rth_ppm_close(st) == 0 && rc == 0) ? 0 : -1;
+}
+
+int rth_ppm_open(const char *path, int W, int H, int threads, rth_ppm_stream **out) {
+    if (!path || !out || W < 0 || H < 0) return -1;
+    *out = nullptr;
     const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd < 0) return -1;
     char head[64];
     const int hn = std::snprintf(head, sizeof head, "P3 \n%d %d \n255 \n", W, H);
-    bool ok = ::pwrite(fd, head, (size_t)hn, 0) == (ssize_t)hn;
-    const size_t npx = (size_t)W * (size_t)H;
-    if (threads <= 0) threads = host_threads();
+    auto *st = new rth_ppm_stream;
+    st->fd = fd;
+    st->W = W;
+    st->H = H;
+    st->rows = 0;
+    st->off = (size_t)hn;
+    st->threads = threads <= 0 ? host_threads() : threads;
+    st->good = ::pwrite(fd, head, (size_t)hn, 0) == (ssize_t)hn;
+    *out = st;
+    return st->good ? 0 : -1;
+}
+
+// The next nrows image rows (nrows * W * 3 floats): every host thread takes
+// chunks of 32 768 pixels in order, formats them (a table for 0..255,
+// std::to_chars for the rest) and pwrites them at their offset, known once
+// every earlier chunk has its length; no thread waits for a single writer.
+int rth_ppm_write_rows(rth_ppm_stream *st, const float *rgb, int nrows) {
+    if (!st || (!rgb && nrows > 0) || nrows < 0 || st->rows + nrows > st->H) return -1;
     static const struct Lut {
         char s[256][4];
         unsigned char n[256];
@@ -634,6 +667,7 @@ int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads)
             }
         }
     } lut;
+    const size_t npx = (size_t)st->W * (size_t)nrows;
     const size_t chunk = 1 << 15;
     const size_t nchunks = (npx + chunk - 1) / chunk;
     std::vector<size_t> len(nchunks, SIZE_MAX);       // formatted length of each chunk
@@ -641,7 +675,7 @@ int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads)
     std::condition_variable cv;
     size_t next = 0;                                  // next chunk to take
     size_t known = 0;                                 // chunks [0, known) have their offsets
-    size_t end_off = (size_t)hn;                      // file offset after chunk known - 1
+    size_t end_off = st->off;                         // file offset after chunk known - 1
     std::vector<size_t> off(nchunks, 0);
     auto format = [&](size_t c, std::string &o) {
         const size_t p0 = c * chunk, p1 = std::min(npx, p0 + chunk);
@@ -662,7 +696,8 @@ int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads)
         }
         o.resize((size_t)(q - o.data()));
     };
-    std::atomic<bool> good{ok};
+    std::atomic<bool> good{true};
+    const int fd = st->fd;
     auto worker = [&] {
         std::string buf;
         for (;;) {
@@ -698,11 +733,21 @@ int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads)
         }
     };
     std::vector<std::thread> pool;
-    const int nt = (int)std::min<size_t>((size_t)threads, std::max<size_t>(1, nchunks));
+    const int nt = (int)std::min<size_t>((size_t)st->threads, std::max<size_t>(1, nchunks));
     for (int t = 1; t < nt; t++) pool.emplace_back(worker);
     worker();
     for (auto &th : pool) th.join();
-    if (::close(fd) != 0) good = false;
+    st->off = end_off;
+    st->rows += nrows;
+    if (!good) st->good = false;
+    return good ? 0 : -1;
+}
+
+int rth_ppm_close(rth_ppm_stream *st) {
+    if (!st) return -1;
+    bool good = st->good && st->rows == st->H;
+    if (::close(st->fd) != 0) good = false;
+    delete st;
     return good ? 0 : -1;
 }
 

@@ -86,7 +86,7 @@ _hip = None
 
 HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_set_imsize",
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
-                "rth_output_path", "rth_row_set"]
+                "rth_output_path", "rth_row_set", "rth_ppm_open", "rth_ppm_write_rows", "rth_ppm_close"]
 HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
@@ -114,6 +114,10 @@ def host_lib() -> C.CDLL:
         L.rth_quantize.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
         L.rth_write_ppm.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
         L.rth_output_path.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        if hasattr(L, "rth_ppm_open"):    # absent from round-1..3 libraries (A/B baselines)
+            L.rth_ppm_open.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+            L.rth_ppm_write_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+            L.rth_ppm_close.argtypes = [C.c_void_p]
         if hasattr(L, "rth_row_set"):     # absent from round-1 libraries (A/B baselines)
             L.rth_row_set.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4
         _host = L
@@ -265,6 +269,23 @@ def write_ppm(path: str, rgb: np.ndarray, threads: int = 0) -> None:
     a = np.ascontiguousarray(rgb, dtype=np.float32)
     H, W = a.shape[:2]
     if host_lib().rth_write_ppm(os.fsencode(path), a.ctypes.data, W, H, threads) != 0:
+        raise RTError(f"cannot write {path}")
+
+
+def write_ppm_blocks(path: str, rgb: np.ndarray, block: int, threads: int = 0) -> None:
+    """The P3 file written in blocks of `block` rows (rth_ppm_open / rth_ppm_write_rows /
+    rth_ppm_close): byte-identical to write_ppm."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    H, W = a.shape[:2]
+    L = host_lib()
+    h = C.c_void_p()
+    if L.rth_ppm_open(os.fsencode(path), W, H, threads, C.byref(h)) != 0:
+        raise RTError(f"cannot open {path}")
+    ok = True
+    for y in range(0, H, block):
+        n = min(block, H - y)
+        ok = L.rth_ppm_write_rows(h, a[y:y + n].ctypes.data, n) == 0 and ok
+    if L.rth_ppm_close(h) != 0 or not ok:
         raise RTError(f"cannot write {path}")
 
 

@@ -100,6 +100,31 @@ def test_writer_large_parallel_matches():
         assert hashlib.md5(open(p, "rb").read()).hexdigest() == hashlib.md5(ppm_bytes(img)).hexdigest()
 
 
+def test_writer_in_row_blocks_matches():
+    """The streaming writer (rth_ppm_open / write_rows / close: the CLI's
+    copy-and-write overlap) gives write_ppm's bytes for any block size,
+    including blocks that do not divide the height and NaN / out-of-range
+    values; a short write (rows missing at close) fails."""
+    rng = np.random.default_rng(9)
+    img = rng.uniform(-0.5, 1.5, size=(67, 131, 3)).astype(np.float32)
+    img[5, 7, 1] = np.nan
+    img[60, 3, 2] = 3e9
+    import tempfile
+    ref = ppm_bytes(img)
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "x.ppm")
+        for block, threads in ((1, 1), (8, 3), (13, 8), (67, 2), (100, 4)):
+            rtamd.write_ppm_blocks(p, img, block, threads)
+            assert open(p, "rb").read() == ref, (block, threads)
+        L = rtamd.host_lib()
+        import ctypes as C
+        h = C.c_void_p()
+        assert L.rth_ppm_open(os.fsencode(p), 131, 67, 2, C.byref(h)) == 0
+        assert L.rth_ppm_write_rows(h, img.ctypes.data, 10) == 0
+        assert L.rth_ppm_write_rows(h, img.ctypes.data, 60) == -1      # past the height
+        assert L.rth_ppm_close(h) == -1                                # 10 of 67 rows
+
+
 def test_output_path_is_remove_extension():
     assert rtamd.output_path("a/b/scene.txt") == "a/b/scene.ppm"
     assert rtamd.output_path("scene") == "scene.ppm"
