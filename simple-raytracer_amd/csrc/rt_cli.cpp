@@ -60,7 +60,8 @@ struct HostImage {
 // HIP error goes to hip_rc.
 int stream_ppm(const char *path, const float *dimg, int W, int H, int &hip_rc) {
     const size_t row = (size_t)W * 3;
-    const int R = (int)std::max<size_t>(1, std::min<size_t>((size_t)H, (size_t(64) << 20) / (row * sizeof(float))));
+    int R = (int)std::max<size_t>(1, std::min<size_t>((size_t)H, (size_t(64) << 20) / (row * sizeof(float))));
+    if (const char *e = std::getenv("RT_PPM_BLOCK_ROWS")) R = std::max(1, std::min(H, std::atoi(e)));   // test hook
     const int nb = (H + R - 1) / R;
     float *pin[2] = {nullptr, nullptr};
     hipStream_t cs = nullptr;

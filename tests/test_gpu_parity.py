@@ -955,6 +955,32 @@ def test_deinterleave_rows_device():
                                       C.c_void_p(img.data_ptr()), None) == -1
 
 
+@pytest.mark.parametrize("block", ["", "1", "7", "64"])
+def test_cli_streamed_ppm_matches(block, tmp_path):
+    """Without --float-out the one-device CLI copies the image to the host in
+    row blocks through pinned buffers and writes each while the next copies
+    (stream_ppm, rth_ppm_*): the P3 file is byte-identical to the one written
+    from the whole float image (--float-out takes that path), for the default
+    block and for 1-, 7- and 64-row blocks (RT_PPM_BLOCK_ROWS) on a ragged
+    image."""
+    name = "test7_s.txt"
+    outs = []
+    for args, env in (([ "--float-out", str(tmp_path / "f.bin")], {}), ([], {"RT_PPM_BLOCK_ROWS": block} if block else {})):
+        tmp_name = "_stream_" + name
+        shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
+        out = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
+        try:
+            r = subprocess.run([CLI, tmp_name] + args, cwd=SCENES, capture_output=True, text=True, timeout=300,
+                               env={**os.environ, **env})
+            assert r.returncode == 0, r.stderr
+            outs.append(open(out, "rb").read())
+        finally:
+            for p in (os.path.join(SCENES, tmp_name), out):
+                if os.path.exists(p):
+                    os.remove(p)
+    assert outs[0] == outs[1] and len(outs[0]) > 1000
+
+
 @pytest.mark.parametrize("name", ["test7_s.txt", "C3_64x64.txt"])
 def test_cli_rccl_gather(name, tmp_path):
     """`rt --gpus 1 --gather rccl`: the image goes through the multi-device
