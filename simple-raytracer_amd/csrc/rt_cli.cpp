@@ -302,8 +302,13 @@ int main(int argc, char *argv[]) {
         if (!r) r = rt_render_rows(s, &cam, W, H, 0, H, dimg, &st[0]);
         ph_render = ms_since(t);
         t = Clock::now();
-        if (!r && !float_out) {
-            // copy and write overlapped (stream_ppm): one phase, reported as the write
+        // copy and write overlapped (stream_ppm) for images of 512 MB and more:
+        // below that the two pinned buffers' allocation costs more than the
+        // overlap saves (C3's 201 MB: 37 -> 96 ms; C5's 3.2 GB: 542 -> 361 ms)
+        const bool stream = (size_t)W * H * 3 * sizeof(float) >= (size_t(512) << 20) ||
+                            std::getenv("RT_PPM_BLOCK_ROWS") != nullptr;
+        if (!r && !float_out && stream) {
+            // one phase, reported as the write
             streamed = true;
             streamed_wr = stream_ppm(out, dimg, W, H, r);
             ph_write = ms_since(t);

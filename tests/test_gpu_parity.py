@@ -955,17 +955,17 @@ def test_deinterleave_rows_device():
                                       C.c_void_p(img.data_ptr()), None) == -1
 
 
-@pytest.mark.parametrize("block", ["", "1", "7", "64"])
+@pytest.mark.parametrize("block", ["100000", "1", "7", "64"])
 def test_cli_streamed_ppm_matches(block, tmp_path):
     """Without --float-out the one-device CLI copies the image to the host in
     row blocks through pinned buffers and writes each while the next copies
-    (stream_ppm, rth_ppm_*): the P3 file is byte-identical to the one written
-    from the whole float image (--float-out takes that path), for the default
-    block and for 1-, 7- and 64-row blocks (RT_PPM_BLOCK_ROWS) on a ragged
-    image."""
+    (stream_ppm, rth_ppm_*; images of 512 MB and more, or whenever
+    RT_PPM_BLOCK_ROWS is set): the P3 file is byte-identical to the one
+    written from the whole float image (--float-out takes that path), for one
+    block and for 1-, 7- and 64-row blocks on a ragged image."""
     name = "test7_s.txt"
     outs = []
-    for args, env in (([ "--float-out", str(tmp_path / "f.bin")], {}), ([], {"RT_PPM_BLOCK_ROWS": block} if block else {})):
+    for args, env in ((["--float-out", str(tmp_path / "f.bin")], {}), ([], {"RT_PPM_BLOCK_ROWS": block})):
         tmp_name = "_stream_" + name
         shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
         out = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
