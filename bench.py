@@ -123,28 +123,42 @@ def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
             "sample": f"{config} scene at {sample}x{sample}, oracle restatement, {dt:.1f} s"}
 
 
-def cpu_port_baseline(config: str, sample: int) -> dict:
+def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0) -> dict:
     """SURVEY.md §8d's CPU path: this repo's C restatement of the reference
     (oracle/rt_oracle.c: the same brute-force TraceRay/ShadeRay), OpenMP over
-    rows on all the threads this process may use (OMP_NUM_THREADS), timed on a
-    sample x sample render of the same seeded scene.  A reported baseline, not
-    the product (the product path has no CPU fallback)."""
+    rows on every core this process may run on (its affinity: all the node's
+    CPUs the lease gives it, not the lease's OMP_NUM_THREADS share), timed on
+    a render of the same seeded scene at a size chosen for ~target_s seconds
+    (a `sample` x `sample` probe first sets the rate; at most the config's
+    own image).  A reported baseline, not the product (the product path has
+    no CPU fallback)."""
     from rtamd import scenes as gen
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_py import OracleScene
-    d = tempfile.mkdtemp(prefix="rtamd_port_")
-    path = gen.write_scene(d, config, w=sample, h=sample, tag=f"{config}_{sample}_port")
-    o = OracleScene(path)
-    o.set_depth(gen.CONFIGS[config]["depth"])
     host = host_cores()
-    threads = host["omp_num_threads"] or host["affinity"]
-    t0 = time.perf_counter()
-    _, cnt = o.render(threads=threads)
-    dt = time.perf_counter() - t0
-    r = sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection"))
+    threads = host["affinity"]
+
+    def run(side: int):
+        d = tempfile.mkdtemp(prefix="rtamd_port_")
+        path = gen.write_scene(d, config, w=side, h=side, tag=f"{config}_{side}_port")
+        o = OracleScene(path)
+        o.set_depth(gen.CONFIGS[config]["depth"])
+        t0 = time.perf_counter()
+        _, cnt = o.render(threads=threads)
+        dt = time.perf_counter() - t0
+        return sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection")), dt
+
+    r, dt = run(sample)
+    full = gen.CONFIGS[config]["w"]
+    side = int(min(full, sample * (target_s / max(dt, 1e-3)) ** 0.5)) // 64 * 64
+    if side > sample:
+        r, dt = run(side)
+    else:
+        side = sample
     return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port", "host": host,
-            "sample": f"{config} scene at {sample}x{sample} (full field of view), {r} rays, {dt:.1f} s, "
-                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows on {threads} threads"}
+            "sample": f"{config} scene at {side}x{side} (full field of view), {r} rays, {dt:.1f} s, "
+                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows on {threads} threads "
+                      f"(the process's affinity)"}
 
 
 def host_cores() -> dict:
@@ -317,6 +331,9 @@ def main() -> None:
         if not verified:
             raise SystemExit(f"verify: gathered image differs from the whole-image render in "
                              f"{int((a != b).any(dim=-1).sum())} pixels")
+    # the last timed frame's image (this rank's rows, as the kernel without
+    # counters rendered them), kept before the frames below reuse the buffers
+    timed_rows = gathers[(args.steps - 1) % F].strip.clone() if nrows > 0 and args.steps > 0 else None
     # single-frame latency (nothing else in flight), after the timed region
     torch.cuda.synchronize()
     lat0 = time.perf_counter()
@@ -334,12 +351,35 @@ def main() -> None:
     # instantiation; the roofline divides its tests by the uncounted launch's
     # time above
     st = st_time
-    if counting and args.count_render == "on":
-        gs.set_option("counters", 1)
-        step(0)
+    verified_rows = None
+    if args.count_render == "on":
+        # the counting render writes a buffer of its own; the timed frame must
+        # equal it bit for bit (NaN for NaN) on every rank: the benched
+        # instantiation is checked on the very frame the line times, against
+        # the instantiation every parity test pins to the oracle
+        if counting:
+            gs.set_option("counters", 1)
+        cnt_rows = torch.empty_like(gathers[0].strip)
+        s0 = torch.cuda.current_stream()
+        if nrows > 0:
+            gs.render_row_blocks_async(cam, W, H, ry0, rblock, rstep, nrows, cnt_rows.data_ptr(), s0.cuda_stream)
         torch.cuda.synchronize()
         st = gs.last_stats()
-        gs.set_option("counters", 0)
+        if counting:
+            gs.set_option("counters", 0)
+        same = True
+        if timed_rows is not None:
+            a = torch.nan_to_num(timed_rows[:nrows], nan=-9.0)
+            b = torch.nan_to_num(cnt_rows[:nrows], nan=-9.0)
+            same = bool(torch.equal(a, b))
+        ok = torch.tensor([1 if same else 0], dtype=torch.int32,
+                          device="cuda" if args.dist_backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        verified_rows = bool(int(ok.item()))
+        del cnt_rows
+        if not verified_rows:
+            raise SystemExit("verify: the last timed frame differs from the counting render of the same rows")
     st_tests = st
     my_rays = st.rays()
 
@@ -387,7 +427,7 @@ def main() -> None:
             except Exception as e:  # never lose the GPU line to the CPU leg
                 cpu = {"error": repr(e)}
             try:
-                cpu_port = cpu_port_baseline(args.config, 4 * args.cpu_sample)
+                cpu_port = cpu_port_baseline(args.config, 2 * args.cpu_sample)
             except Exception as e:
                 cpu_port = {"error": repr(e)}
         line = {
@@ -454,7 +494,12 @@ def main() -> None:
                                  "frac": round(alg_bytes / k_s / 1e9 / PEAK_HBM_GBPS, 7)}},
             "cpu_baseline": cpu,
             "cpu_port": cpu_port,
-            "verified": verified,
+            "verified": verified_rows,
+            "verified_note": "every rank's rows of the last timed frame (render_kernel without counters) equal "
+                             "bit for bit (NaN for NaN) the counting instantiation's render of the same rows, "
+                             "which the parity tests pin to the oracle"
+                             + ("; --verify: the gathered image equals one whole-image render" if verified
+                                else ""),
             "ray_counts": {k: int(getattr(st, k)) for k in ("primary", "shadow", "refraction",
                                                              "reflection", "skip_trans", "ub_back")},
         }

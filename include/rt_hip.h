@@ -137,13 +137,27 @@ typedef struct rt_scene rt_scene;
 
 int rt_device_count(void);
 
+/* Optional: start the HIP runtime and the state it makes lazily on first use
+ * for `device` -- the context, device memory, the copy paths, a hardware queue
+ * (a stream the next rt_scene_create on the device takes), the kernels' code
+ * object -- ahead of rt_scene_create, e.g. on a thread while the scene file
+ * is parsed (the CLI does: ~40-50 ms that would otherwise land in the first
+ * scene upload and the first stats read).  Thread-safe; may be called again. */
+int rt_device_init(int device);
+
 /* Upload a scene to HIP device `device`. */
 int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out);
 int rt_scene_destroy(rt_scene *scene);
 
 /* Render image rows [y0, y1) of a W x H image into out_rgb, which holds
  * (y1 - y0) * W * 3 floats (row-major, RGB) and may be host or device
- * memory.  Synchronous.  stats may be NULL. */
+ * memory.  Synchronous.  stats may be NULL.  W, H >= 1: the seam itself
+ * (main.cpp:670) takes any size -- a 1-pixel-wide or -tall image divides by
+ * res - 1 = 0 (main.cpp:709-710), its camera deltas are NaN / inf
+ * (rth_camera does the same), every primary ray is NaN and meets nothing, and
+ * every pixel is the background, as in the reference.  (The reference's
+ * parser rejects such an imsize before the seam, main.cpp:242; so does
+ * rt_host.h's.) */
 int rt_render_rows(rt_scene *scene, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb,
                    rt_stats *stats);
 
@@ -235,6 +249,14 @@ int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *
  * 64 nodes and their leaves, each wave starting its searches in one of them --
  * spreads the reads every search makes of the root over L2 channels; never
  * changes the image),
+ * "counters" (1, the default: the kernel instantiation that counts rays and
+ * executed tests for rt_stats; 0: the one without counters, which bench.py
+ * times -- its stats report no rays; never changes the image),
+ * "last_light_skip" (-1 auto, 0 off: a last light whose Phong term is exactly
+ * 0 is counted but not searched, in scenes where that is exact -- never
+ * changes the image), "recursive" (test hook: 1 renders a scene without
+ * reflecting / refracting materials with the recursive instantiation instead
+ * of the MAXF = 1 one -- never changes the image),
  * "fail_bvh_upload" (test hook: 1 makes BVH uploads fail with RT_E_NOMEM). */
 int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
 
@@ -253,8 +275,11 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * bits in effect (option org_first), [41] the scene's density (objects a line
  * across it meets, x1000), [42] BVH stack entries in LDS, [43] lights staged
  * in LDS (1) or read from device memory (0), [44] copies of the BVH's top in
- * effect (option hot_copies), [45] work bands (option work_parts).
- * n <= 48. */
+ * effect (option hot_copies; on the device this slot counts the ub_back
+ * events, which rt_scene_debug_ub_pixels returns), [45] work bands (option
+ * work_parts), [48] the counting kernel instantiation (option counters: 1)
+ * or the one without counters (0); RT_CHECK builds: [49] stack-bottom
+ * invariant violations (must be 0).  n <= 64. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);
 
 /* The last render's back() reads of an empty medium stack (main.cpp:1028,

@@ -63,6 +63,14 @@ int rth_ppm_open(const char *path, int W, int H, int threads, rth_ppm_stream **o
 int rth_ppm_write_rows(rth_ppm_stream *stream, const float *rgb, int nrows);
 int rth_ppm_close(rth_ppm_stream *stream);
 
+/* The same file from the pixel values as bytes (W * H * 3, or nrows * W * 3
+ * for a row block) -- what rt_hip.h's rt_quantize_u8 makes on the device when
+ * every value is 0..255 (its flag clear): byte-identical to rth_write_ppm /
+ * rth_ppm_write_rows of the floats they came from.  The CLI copies these
+ * 3 bytes per pixel to the host instead of 12.  Each returns 0 or -1. */
+int rth_write_ppm_u8(const char *path, const unsigned char *v, int W, int H, int threads);
+int rth_ppm_write_rows_u8(rth_ppm_stream *stream, const unsigned char *v, int nrows);
+
 /* remove_extension(path) + ".ppm" (src/utility.h:34-41, main.cpp:614-616). */
 int rth_output_path(const char *scene_path, char *out, int outlen);
 

@@ -66,7 +66,7 @@ bool build_wide(const AccelOpts &o, int threads, std::vector<rtbvh::Prim> &P, rt
 // finite, or the scene is so large that one ulp of B reaches epsilon (then
 // the h < 0 side is no longer safe): the caller falls back to the scan.
 bool dir_tree(const AccelInput &in, const AccelOpts &o, int threads, const LightK &lt, double D,
-              std::vector<rtbvh::Node4H> &nodes, std::vector<float4> &rec, DirK &out, int &max_stack) {
+              std::vector<rtbvh::NodeDev> &nodes, std::vector<float4> &rec, DirK &out, int &max_stack) {
     for (int k = 0; k < 9; k++) out.R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
     out.root = -1;
     out.cone_k = 0.0f;
@@ -135,7 +135,7 @@ bool dir_tree(const AccelInput &in, const AccelOpts &o, int threads, const Light
             return 2;
         },
         rec.size());
-    std::vector<rtbvh::Node4H> QQ;
+    std::vector<rtbvh::NodeDev> QQ;
     if (!ok || !rtbvh::quantize(Q, QQ, threads)) return false;
     const int base = (int)nodes.size();
     for (auto &z : QQ) {
@@ -380,7 +380,7 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
             }
     out.ms[3] = ms_since(t0);
     t0 = Clock::now();
-    std::vector<rtbvh::Node4H> &QQ = out.nodes;
+    std::vector<rtbvh::NodeDev> &QQ = out.nodes;
     if (ok && !Q.nodes.empty() && !rtbvh::quantize(Q, QQ, threads)) ok = false;   // non-finite geometry: scan
     for (auto &z : QQ)                                  // device form: unused slot -> the empty leaf
         for (auto &l : z.link)
@@ -410,18 +410,18 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
     // device links: an inner node's link is its byte offset in the node array
     // (the kernel fetches a node with buffer loads at that offset: no address
     // arithmetic per visit), leaf links stay as they are
-    if (ok && QQ.size() * sizeof(rtbvh::Node4H) > (size_t)INT32_MAX) ok = false;
+    if (ok && QQ.size() * sizeof(rtbvh::NodeDev) > (size_t)INT32_MAX) ok = false;
     if (ok) {
         for (auto &z : QQ)
             for (auto &l : z.link)
-                if (l >= 0) l *= (int32_t)sizeof(rtbvh::Node4H);
+                if (l >= 0) l *= (int32_t)sizeof(rtbvh::NodeDev);
         for (auto &d : out.dirk)
-            if (d.root >= 0) d.root *= (int)sizeof(rtbvh::Node4H);
+            if (d.root >= 0) d.root *= (int)sizeof(rtbvh::NodeDev);
     }
     // hot copies of the main tree's top (rt_accel.h, kHotNodes)
     const int K = o.hot_copies;
     if (ok && K > 1 && (K & (K - 1)) == 0 && !Q.nodes.empty()) {
-        const size_t nb = sizeof(rtbvh::Node4H);
+        const size_t nb = sizeof(rtbvh::NodeDev);
         const int M = (int)std::min<size_t>(Q.nodes.size(), (size_t)kHotNodes);
         auto up = [](size_t v, size_t a) { return (v + a - 1) / a * a; };
         out.hot_copies = K;
@@ -435,7 +435,9 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
                 if (l < 0 && l != rtbvh::kEmptyLeaf && std::find(leaves.begin(), leaves.end(), l) == leaves.end())
                     leaves.push_back(l);
         rec.resize(rec.size() - 3);                    // the padding goes after the copies
-        for (int c = 0; c < K && ok; c++) {
+        const size_t rec_main = rec.size();            // the main and cone trees' records end here
+        bool hot_ok = true;                            // a failed copy drops the copies, not the tree
+        for (int c = 0; c < K && hot_ok; c++) {
             // this copy's records (16-word aligned + 16: another channel again)
             rec.resize(up(rec.size(), 16) + (c ? 16 : 0), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
             std::vector<int32_t> remap(leaves.size());
@@ -445,7 +447,7 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
                 const size_t words = 5 * (size_t)nfc + 2 * (size_t)(cnt - nfc);
                 const size_t noff = rec.size();
                 if (noff + words >= (size_t(1) << 23) - 1) {
-                    ok = false;
+                    hot_ok = false;
                     break;
                 }
                 rec.resize(noff + words);
@@ -453,8 +455,8 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
                 remap[k] = -(1 + (int32_t)((noff << 8) | (size_t)(nfc << 4) | (size_t)cnt));
             }
             const size_t cbase = out.hot_base + (size_t)c * out.hot_stride;
-            for (int i = 0; i < M && ok; i++) {
-                rtbvh::Node4H z = QQ[i];
+            for (int i = 0; i < M && hot_ok; i++) {
+                rtbvh::NodeDev z = QQ[i];
                 for (int32_t &l : z.link) {
                     if (l >= 0) {
                         const size_t child = (size_t)l / nb;    // main-array index
@@ -466,12 +468,16 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
                 out.hot_nodes.push_back(z);
             }
         }
-        rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        if (!ok || out.hot_base + (size_t)K * out.hot_stride > (size_t)INT32_MAX) {
-            ok = false;
+        if (!hot_ok || out.hot_base + (size_t)K * out.hot_stride > (size_t)INT32_MAX) {
+            // the copies do not fit the link encoding: the main tree (valid
+            // before they were appended) renders without them, not the scan
+            rec.resize(rec_main);
             out.hot_copies = 0;
+            out.hot_per_copy = 0;
+            out.hot_base = out.hot_stride = 0;
             out.hot_nodes.clear();
         }
+        rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     }
     out.ok = ok;
     out.dir_mode = dir_mode;

@@ -75,7 +75,7 @@ constexpr int kHotNodes = 64;
 // The device's trees, ready to upload.
 struct AccelTree {
     bool ok = false;                   // false: geometry the BVH cannot bound (the scan is used)
-    std::vector<rtbvh::Node4H> nodes;  // main tree first, then the cone trees; links are byte offsets
+    std::vector<rtbvh::NodeDev> nodes;  // main tree first, then the cone trees; links are byte offsets
     std::vector<float4> rec;           // leaf records (rt_bvh.h leaf_records), padded by 3 words
     std::vector<int32_t> objleaf;      // per object: its leaf's link in the main tree
     std::vector<DirK> dirk;            // per light (directional lights only)
@@ -89,7 +89,7 @@ struct AccelTree {
     // in order (hot_per_copy each); their records are appended to rec
     int hot_copies = 0, hot_per_copy = 0;
     size_t hot_base = 0, hot_stride = 0;
-    std::vector<rtbvh::Node4H> hot_nodes;
+    std::vector<rtbvh::NodeDev> hot_nodes;
     // host time per phase (ms): primitive boxes, binary SAH build, collapse +
     // BFS order, leaf records, quantisation, cone trees
     double ms[6] = {0, 0, 0, 0, 0, 0};

@@ -17,7 +17,9 @@
 // the host clock: parse, scene upload, BVH build, render, device->host copy,
 // quantise + P3 write; '-' = stderr).
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
@@ -102,6 +104,71 @@ int stream_ppm(const char *path, const float *dimg, int W, int H, int &hip_rc) {
     }
     if (cs) (void)hipStreamDestroy(cs);
     return wr;
+}
+
+// One device, P3 out from the writer's pixel values as bytes: the device
+// quantises the image (rt_quantize_u8, exact for values 0..255), row blocks
+// of ~16 MB of bytes come to the host on a copier thread, and the writer
+// formats each block (rth_ppm_write_rows_u8) as soon as it has landed --
+// 3 bytes per pixel cross PCIe instead of 12, and the copy hides behind the
+// writer.  Returns 1 when some value is not 0..255 (NaN, a background above
+// 1: the floats must be written, nothing was written), else 0 on success or
+// -1 on a write error; a HIP error goes to hip_rc.  d2h_ms: the copier's time.
+int write_ppm_bytes(const char *path, const float *dimg, int W, int H, int &hip_rc, double &d2h_ms) {
+    const size_t n = (size_t)W * H * 3, row = (size_t)W * 3;
+    unsigned char *d8 = nullptr;
+    unsigned *dflag = nullptr;
+    unsigned flag = 0;
+    if (hipMalloc((void **)&d8, std::max<size_t>(4, (n + 3) / 4 * 4)) != hipSuccess ||
+        hipMalloc((void **)&dflag, sizeof(unsigned)) != hipSuccess ||
+        hipMemset(dflag, 0, sizeof(unsigned)) != hipSuccess || rt_quantize_u8(dimg, (long long)n, d8, dflag, nullptr) ||
+        hipMemcpy(&flag, dflag, sizeof flag, hipMemcpyDeviceToHost) != hipSuccess) {
+        hip_rc = RT_E_HIP;
+    }
+    int ret = 0;
+    if (!hip_rc && (flag & 1u)) ret = 1;
+    if (!hip_rc && ret == 0) {
+        std::unique_ptr<unsigned char[]> host(new unsigned char[n]);
+        int R = (int)std::max<size_t>(1, std::min<size_t>((size_t)H, (size_t(16) << 20) / std::max<size_t>(1, row)));
+        if (const char *e = std::getenv("RT_PPM_BLOCK_ROWS")) R = std::max(1, std::min(H, std::atoi(e)));   // test hook
+        const int nb = (H + R - 1) / R;
+        std::mutex mu;
+        std::condition_variable cv;
+        int landed = 0;                    // blocks [0, landed) are on the host
+        bool failed = false;
+        const auto t0 = Clock::now();
+        std::thread copier([&] {
+            for (int b = 0; b < nb; b++) {
+                const size_t r0 = (size_t)b * R, rows = std::min<size_t>(R, H - r0);
+                const bool ok = hipMemcpy(host.get() + r0 * row, d8 + r0 * row, rows * row, hipMemcpyDeviceToHost) ==
+                                hipSuccess;
+                std::lock_guard<std::mutex> lk(mu);
+                if (!ok) failed = true;
+                landed = ok ? b + 1 : nb;
+                cv.notify_all();
+                if (!ok) break;
+            }
+            d2h_ms = ms_since(t0);
+        });
+        rth_ppm_stream *ps = nullptr;
+        bool good = rth_ppm_open(path, W, H, 0, &ps) == 0;
+        for (int b = 0; b < nb; b++) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return landed > b; });
+                if (failed) break;
+            }
+            const int rows = std::min(R, H - b * R);
+            if (good && rth_ppm_write_rows_u8(ps, host.get() + (size_t)b * R * row, rows) != 0) good = false;
+        }
+        copier.join();
+        if (failed) hip_rc = RT_E_HIP;
+        if (ps && rth_ppm_close(ps) != 0) good = false;
+        ret = good ? 0 : -1;
+    }
+    if (d8) (void)hipFree(d8);
+    if (dflag) (void)hipFree(dflag);
+    return ret;
 }
 
 // The kernel instantiation with counters (rays by kind, executed tests)
@@ -221,11 +288,26 @@ int main(int argc, char *argv[]) {
     }
     // phases of the one-shot run (--stats-json), host clock
     double ph_parse = 0, ph_create = 0, ph_bvh = 0, ph_render = 0, ph_d2h = 0, ph_write = 0;
+    // The HIP runtime and the device's context start on a thread of their
+    // own while the scene file is parsed (C5's 11 MB: ~35 ms, HIP's start
+    // 50-130 ms): neither needs the other
+    int ndev = 0;
+    double init_ms = 0.0;
+    std::thread hip_init([&] {
+        const auto ti = Clock::now();
+        ndev = rt_device_count();                // the HIP runtime starts here
+        // and the device's lazily made state (rt_device_init: context, memory,
+        // copy paths, a hardware queue, the code object), for every device used
+        for (int g = 0; g < std::max(1, gpus) && device + g < ndev; g++)
+            if (device + g >= 0) (void)rt_device_init(device + g);
+        init_ms = ms_since(ti);
+    });
     auto t = Clock::now();
     rth_scene *hs = nullptr;
     std::vector<char> msg(1 << 16);
     int rc = rth_parse_file(argv[1], &hs, msg.data(), (int)msg.size());
     ph_parse = ms_since(t);
+    if (rc != 0) hip_init.join();
     if (rc > 0) {
         std::cout << msg.data() << std::endl;
         return 0;
@@ -246,8 +328,8 @@ int main(int argc, char *argv[]) {
     rth_camera(hs, W, H, &cam);
 
     t = Clock::now();
-    int ndev = rt_device_count();                // the HIP runtime starts here
-    const double ph_hip_init = ms_since(t);
+    hip_init.join();
+    const double ph_hip_init = ms_since(t);      // what the parse did not hide of init_ms
     if (ndev < 1) {
         std::cerr << "rt: no HIP device" << std::endl;
         return 2;
@@ -270,8 +352,10 @@ int main(int argc, char *argv[]) {
     rth_output_path(argv[1], out, sizeof out);
     HostImage img((size_t)W * H * 3);
     double ph_count = 0.0;                 // the counting render (--stats*): not a phase of the run
-    bool streamed = false;                 // one device, no --float-out: stream_ppm wrote the file
+    bool streamed = false;                 // one device: write_ppm_bytes or stream_ppm wrote the file
     int streamed_wr = 0;
+    bool d2h_overlapped = false;           // the copy ran under the writer (its time is inside the write)
+    const char *ppm_from = "floats";       // what the writer formatted: device-quantised bytes or floats
     const double ph_alloc = ms_since(t);
     std::vector<rt_stats> st(gpus);
     std::vector<int> rcs(gpus, 0);
@@ -302,22 +386,42 @@ int main(int argc, char *argv[]) {
         if (!r) r = rt_render_rows(s, &cam, W, H, 0, H, dimg, &st[0]);
         ph_render = ms_since(t);
         t = Clock::now();
-        // copy and write overlapped (stream_ppm) for images of 512 MB and more:
-        // below that the two pinned buffers' allocation costs more than the
-        // overlap saves (C3's 201 MB: 37 -> 96 ms; C5's 3.2 GB: 542 -> 361 ms)
+        // the writer's values as bytes, quantised on the device (3 B per
+        // pixel to the host, copy overlapped with the writer); the floats
+        // only when some value is not 0..255 or --float-out wants them
+        int bytes_rc = 1;
+        if (!r && !float_out && !std::getenv("RT_PPM_FLOATS")) {
+            double d2h = 0.0;
+            bytes_rc = write_ppm_bytes(out, dimg, W, H, r, d2h);
+            if (bytes_rc != 1) {           // written (or failed): one phase, reported as the write
+                streamed = true;
+                streamed_wr = bytes_rc;
+                ph_write = ms_since(t);
+                ph_d2h = d2h;
+                d2h_overlapped = true;
+            }
+        }
+        t = Clock::now();
+        // floats: copy and write overlapped (stream_ppm) for images of 512 MB
+        // and more: below that the two pinned buffers' allocation costs more
+        // than the overlap saves (C3's 201 MB: 37 -> 96 ms; C5's 3.2 GB: 542 ->
+        // 361 ms)
         const bool stream = (size_t)W * H * 3 * sizeof(float) >= (size_t(512) << 20) ||
                             std::getenv("RT_PPM_BLOCK_ROWS") != nullptr;
-        if (!r && !float_out && stream) {
+        if (streamed || r) {
+        } else if (!float_out && stream) {
             // one phase, reported as the write
             streamed = true;
             streamed_wr = stream_ppm(out, dimg, W, H, r);
             ph_write = ms_since(t);
             ph_d2h = 0.0;
+            d2h_overlapped = true;
         } else {
-            if (!r && hipMemcpy(img.data(), dimg, img.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+            if (hipMemcpy(img.data(), dimg, img.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
                 r = RT_E_HIP;
             ph_d2h = ms_since(t);
         }
+        ppm_from = bytes_rc == 1 ? "floats" : "bytes";
         // --stats / --stats-json: the counts from one more render by the
         // counting instantiation, outside the phases (its image is the same)
         if (!r && g_counters) {
@@ -412,14 +516,14 @@ int main(int argc, char *argv[]) {
         if (f) {
             fprintf(f,
                     "{\"scene\": \"%s\", \"imsize\": [%d, %d], \"depth\": %d, \"gpus\": %d, \"gather\": \"%s\", "
-                    "\"rays\": %llu, \"phases_ms\": {\"parse\": %.3f, \"hip_init\": %.3f, \"host_image_alloc\": %.3f, "
+                    "\"rays\": %llu, \"hip_init_thread_ms\": %.3f, \"phases_ms\": {\"parse\": %.3f, \"hip_init\": %.3f, \"host_image_alloc\": %.3f, "
                     "\"scene_upload\": %.3f, \"bvh_build\": %.3f, "
                     "\"bvh_build_host\": %.3f, \"render\": %.3f, \"kernel\": %.3f, \"d2h\": %.3f, "
-                    "\"quantise_ppm_write\": %.3f}, \"d2h_overlapped_with_write\": %s, \"count_render_ms\": %.3f, "
+                    "\"quantise_ppm_write\": %.3f}, \"d2h_overlapped_with_write\": %s, \"ppm_from\": \"%s\", \"count_render_ms\": %.3f, "
                     "\"total_ms\": %.3f, \"ppm_bytes\": %lld, "
                     "\"Mrays_per_s_end_to_end\": %.3f, \"Mrays_per_s_kernel\": %.3f}\n",
-                    argv[1], W, H, eff_depth, gpus, gather.c_str(), rays, ph_parse, ph_hip_init, ph_alloc, ph_create, ph_bvh, bvh_host, ph_render,
-                    kms, ph_d2h, ph_write, streamed ? "true" : "false", ph_count, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
+                    argv[1], W, H, eff_depth, gpus, gather.c_str(), rays, init_ms, ph_parse, ph_hip_init, ph_alloc, ph_create, ph_bvh, bvh_host, ph_render,
+                    kms, ph_d2h, ph_write, d2h_overlapped ? "true" : "false", ppm_from, ph_count, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
             if (f != stderr) fclose(f);
         }
     }

@@ -146,6 +146,11 @@ enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
 #ifndef RT_PRIO
 #define RT_PRIO 1                        // 1: shading steps at wave priority 2 (render_kernel)
 #endif
+#ifndef RT_CHECK
+#define RT_CHECK 0                       // 1: check the BVH stack-bottom invariant (lib_check/, never benched):
+                                         // violations counted in stats[kCheckSlot]
+#endif
+constexpr int kCheckSlot = 49;
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 5                   // waves per SIMD the register budget must allow (A/B: 5 best)
 #endif
@@ -231,9 +236,9 @@ int maxf_for_depth(int depth);
 // the instantiation for a scene: 1 when no material reflects or refracts (or
 // depth 0), else by depth (-1: deeper than supported)
 int maxf_for(int depth, bool secondary);
-// resident workgroups per CU of render_kernel<maxf, mode> with `lds_bytes` of
-// dynamic LDS (0 if it cannot launch)
-int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes);
+// resident workgroups per CU of render_kernel<maxf, mode, count> with
+// `lds_bytes` of dynamic LDS (0 if it cannot launch)
+int render_blocks_per_cu(int maxf, int mode, bool count, size_t lds_bytes);
 // bytes of one lane's cold ShadeRay frame (Cold<maxf>)
 size_t cold_frame_bytes(int maxf);
 // rt_quantize_u8 (rgb: n floats, 16-B aligned; out: n bytes, 4-B aligned)

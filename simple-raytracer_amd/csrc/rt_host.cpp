@@ -589,7 +589,7 @@ int rth_height(const rth_scene *s) { return s->height; }
 
 // main.cpp:607 (normalised view vectors) + :677-710
 int rth_camera(const rth_scene *s, int W, int H, rt_camera *cam) {
-    if (!s || !cam || W < 2 || H < 2) return RT_E_INVALID;
+    if (!s || !cam || W < 1 || H < 1) return RT_E_INVALID;
     const double kPi = 3.14159265358979323846;  // src/config.h:11
     const double kD = 5.0;                      // src/config.h:8
     F3 n = unit(s->viewdir), up = unit(s->updir);
@@ -650,12 +650,17 @@ int rth_ppm_open(const char *path, int W, int H, int threads, rth_ppm_stream **o
     return st->good ? 0 : -1;
 }
 
-// The next nrows image rows (nrows * W * 3 floats): every host thread takes
-// chunks of 32 768 pixels in order, formats them (a table for 0..255,
-// std::to_chars for the rest) and pwrites them at their offset, known once
-// every earlier chunk has its length; no thread waits for a single writer.
-int rth_ppm_write_rows(rth_ppm_stream *st, const float *rgb, int nrows) {
-    if (!st || (!rgb && nrows > 0) || nrows < 0 || st->rows + nrows > st->H) return -1;
+}  // extern "C"
+
+namespace {
+
+// The next nrows image rows: every host thread takes chunks of 32 768
+// pixels in order, formats them (a table for 0..255, std::to_chars for the
+// rest) and pwrites them at their offset, known once every earlier chunk has
+// its length; no thread waits for a single writer.  value(i) is the i-th
+// value's size_t (rth_quantize of a float, or a byte the device quantised).
+template <class Value>
+int ppm_write_rows(rth_ppm_stream *st, int nrows, Value value) {
     static const struct Lut {
         char s[256][4];
         unsigned char n[256];
@@ -683,7 +688,7 @@ int rth_ppm_write_rows(rth_ppm_stream *st, const float *rgb, int nrows) {
         char *q = o.data();
         for (size_t p = p0; p < p1; p++) {
             for (int k = 0; k < 3; k++) {
-                const unsigned long long v = (unsigned long long)quantize1(rgb[p * 3 + k]);
+                const unsigned long long v = value(p * 3 + k);
                 if (v < 256) {
                     std::memcpy(q, lut.s[v], 4);
                     q += lut.n[v];
@@ -741,6 +746,27 @@ int rth_ppm_write_rows(rth_ppm_stream *st, const float *rgb, int nrows) {
     st->rows += nrows;
     if (!good) st->good = false;
     return good ? 0 : -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rth_ppm_write_rows(rth_ppm_stream *st, const float *rgb, int nrows) {
+    if (!st || (!rgb && nrows > 0) || nrows < 0 || st->rows + nrows > st->H) return -1;
+    return ppm_write_rows(st, nrows, [rgb](size_t i) { return (unsigned long long)quantize1(rgb[i]); });
+}
+
+int rth_ppm_write_rows_u8(rth_ppm_stream *st, const unsigned char *v, int nrows) {
+    if (!st || (!v && nrows > 0) || nrows < 0 || st->rows + nrows > st->H) return -1;
+    return ppm_write_rows(st, nrows, [v](size_t i) { return (unsigned long long)v[i]; });
+}
+
+int rth_write_ppm_u8(const char *path, const unsigned char *v, int W, int H, int threads) {
+    rth_ppm_stream *st = nullptr;
+    if (rth_ppm_open(path, W, H, threads, &st) != 0) return -1;
+    const int rc = rth_ppm_write_rows_u8(st, v, H);
+    return (rth_ppm_close(st) == 0 && rc == 0) ? 0 : -1;
 }
 
 int rth_ppm_close(rth_ppm_stream *st) {

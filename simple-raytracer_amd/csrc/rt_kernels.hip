@@ -276,6 +276,7 @@ __device__ __forceinline__ f4v bldv(__amdgpu_buffer_rsrc_t r, int off, int imm) 
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int off, int imm) { return f4(bldv(r, off, imm)); }
 
 static_assert(sizeof(rtbvh::Node4H) == 104 + 4 * RT_NODE_PAD && rtbvh::kNodeAxisOff == 16 && rtbvh::kNodeLinkOff == 88, "node layout");
+static_assert(sizeof(rtbvh::Node4Q) == 64 && rtbvh::kNodeQLinkOff == 48, "node8 layout");
 // uniform float4 at a byte offset (4-byte aligned), via the scalar unit
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ float4 sld4b(const void *p, int off) {
@@ -444,6 +445,46 @@ __device__ __forceinline__ float4 near_first(float4 w, bool neg) {
     return neg ? make_float4(w.z, w.w, w.x, w.y) : w;
 }
 
+// The same six plane distances from a 64-B node (rt_bvh.h Node4Q, RT_NODE8):
+// w0 = (o_x, o_y, o_z, S_x), w1 = (S_y, S_z, lo_x, hi_x), w2 = (lo_y, hi_y,
+// lo_z, hi_z), S_a = s_a 2^24; child i's q in byte i of a plane dword.  A
+// byte q, moved into a binary16 half (bits 0-7 of either half, the rest 0),
+// is the subnormal q 2^-24, which v_fma_mix_f32 converts exactly inside the
+// plane FMA: t = fma(q 2^-24, S_a / d_a, (o_a - org_a) / d_a).  Per axis the
+// ray's octant picks the near / far dword (m_a: all ones for a negative
+// direction; one v_bfi each), then one mask (children 0, 2) and one permute
+// (children 1, 3) per dword put the bytes in place -- 12 VALU per node visit
+// more than the binary16 windows, for one 16-B load and 40 bytes less.
+__device__ __forceinline__ unsigned bsel(unsigned m, unsigned a, unsigned b) { return (m & a) | (~m & b); }
+__device__ __forceinline__ ChildPlanes child_planes8(float4 w0, float4 w1, float4 w2, float ix, float iy, float iz,
+                                                     float ox, float oy, float oz, unsigned mx, unsigned my,
+                                                     unsigned mz) {
+    const float A[3] = {ix * w0.w, iy * w1.x, iz * w1.y};
+    const float B[3] = {fmaf(w0.x, ix, -ox), fmaf(w0.y, iy, -oy), fmaf(w0.z, iz, -oz)};
+    const unsigned L[3] = {__float_as_uint(w1.z), __float_as_uint(w2.x), __float_as_uint(w2.z)};
+    const unsigned H[3] = {__float_as_uint(w1.w), __float_as_uint(w2.y), __float_as_uint(w2.w)};
+    const unsigned M[3] = {mx, my, mz};
+    ChildPlanes cp;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const unsigned nw = bsel(M[a], H[a], L[a]), fw = bsel(M[a], L[a], H[a]);
+        // children 0, 2 (bytes 0, 2) and 1, 3 (bytes 1, 3) as binary16 pairs
+        const h2v n02 = __builtin_bit_cast(h2v, nw & 0x00ff00ffu);
+        const h2v n13 = __builtin_bit_cast(h2v, __builtin_amdgcn_perm(0u, nw, 0x0c030c01u));
+        const h2v f02 = __builtin_bit_cast(h2v, fw & 0x00ff00ffu);
+        const h2v f13 = __builtin_bit_cast(h2v, __builtin_amdgcn_perm(0u, fw, 0x0c030c01u));
+        cp.tn[a][0] = fmaf((float)n02[0], A[a], B[a]);
+        cp.tn[a][1] = fmaf((float)n13[0], A[a], B[a]);
+        cp.tn[a][2] = fmaf((float)n02[1], A[a], B[a]);
+        cp.tn[a][3] = fmaf((float)n13[1], A[a], B[a]);
+        cp.tf[a][0] = fmaf((float)f02[0], A[a], B[a]);
+        cp.tf[a][1] = fmaf((float)f13[0], A[a], B[a]);
+        cp.tf[a][2] = fmaf((float)f02[1], A[a], B[a]);
+        cp.tf[a][3] = fmaf((float)f13[1], A[a], B[a]);
+    }
+    return cp;
+}
+
 // Sort key of a child: the bits of its entry distance, kMissKey for a miss or
 // an empty slot (unused slots link to the empty leaf, kEmptyLeaf: entering one
 // is harmless, so no link test; their inverted boxes miss anyway).  The entry
@@ -486,17 +527,24 @@ __device__ __forceinline__ unsigned child_entry(const ChildPlanes &cp, int i, fl
 template <bool point, unsigned LEAF_WAIT = kLeafWait, class CNT>
 __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool org_pass = false, int root = 0,
                           V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
-    // |1/d| capped at 2^100 (1/0 -> 2^100): the quantised planes'
-    // 2^e * (1/d) then never overflows (the builder keeps e <= kQExpMax = 27),
-    // and the cap is conservative: an axis with |d| < 2^-100 moves the ray by
-    // less than 2^-100 D along it, far inside the 2^-16 D primitive padding
-    const float ix = point ? 1.0f : clampr(safe_rcp(q.d.x), -0x1p100f, 0x1p100f);
-    const float iy = point ? 1.0f : clampr(safe_rcp(q.d.y), -0x1p100f, 0x1p100f);
-    const float iz = point ? 1.0f : clampr(safe_rcp(q.d.z), -0x1p100f, 0x1p100f);
+    // |1/d| capped at 2^100 (Node4H) or 2^64 (Node4Q; 1/0 -> the cap): the
+    // quantised planes' scale * (1/d) then never overflows (the builder keeps
+    // e <= kQExpMax = 27, or s_a < kQ8ScaleMax = 2^38), and the cap is
+    // conservative: an axis with |d| below 1/cap moves the ray by less than
+    // D / cap along it, far inside the 2^-16 D primitive padding
+    constexpr float kCap = RT_NODE8 ? 0x1p64f : 0x1p100f;
+    const float ix = point ? 1.0f : clampr(safe_rcp(q.d.x), -kCap, kCap);
+    const float iy = point ? 1.0f : clampr(safe_rcp(q.d.y), -kCap, kCap);
+    const float iz = point ? 1.0f : clampr(safe_rcp(q.d.z), -kCap, kCap);
     const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
+#if RT_NODE8
+    // per axis: all ones when the direction is negative (near planes = upper bounds)
+    const unsigned m_x = neg_x ? ~0u : 0u, m_y = neg_y ? ~0u : 0u, m_z = neg_z ? ~0u : 0u;
+#else
     // per axis: the byte offset of the window with the near planes first
     // (rt_bvh.h Node4H: lo lo hi hi lo lo -- word 2 on for a negative direction)
     const int wo_x = neg_x ? 8 : 0, wo_y = neg_y ? 8 : 0, wo_z = neg_z ? 8 : 0;
+#endif
     const float ox = point ? po.x : q.o.x * ix, oy = point ? po.y : q.o.y * iy, oz = point ? po.z : q.o.z * iz;
     const float tlo = point ? 0.0f : q.tmin - fabsf(q.tmin) * 0x1p-16f;
     // directional shadow ray in a scene with spheres: this pass tests the
@@ -531,9 +579,24 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     auto ovf_lane = [&]() -> int * {
         return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * p.ovf_stride;
     };
+    // RT_CHECK builds (lib_check/, not the benched library): the stack-bottom
+    // invariant -- entry 0 is kEmpty, or kRefill + b with 1 <= b blocks in
+    // the lane's spill area (b * kSpill <= ovf_stride) -- at every traversal
+    // entry and exit, spill and refill; a violation is counted
+    // (stats[kCheckSlot], rt_scene_debug_counters [49]) and the access it
+    // would make is skipped
+    auto check = [&](bool ok) -> bool {
+        if (RT_CHECK && !ok) atomicAdd(&p.stats[kCheckSlot], 1ull);
+        return !RT_CHECK || ok;
+    };
+    auto bottom_ok = [&](int tag) {
+        return tag == rtbvh::kEmpty || (tag > kRefill && (tag - kRefill) * kSpill <= p.ovf_stride);
+    };
+    if (RT_CHECK) (void)check(stk[0] == rtbvh::kEmpty);
     auto spill = [&]() {                       // move the oldest kSpill entries out
         const int tag = stk[0];
         const int nb = tag == rtbvh::kEmpty ? 0 : tag - kRefill;
+        if (!check(bottom_ok(tag) && (nb + 1) * kSpill <= p.ovf_stride && sp <= p.stack_cap)) return;
         int *o = ovf_lane() + nb * kSpill;
         for (int i = 0; i < kSpill; i++) o[i] = stk[(1 + i) * kBlock];
         for (int i = kSpill + 1; i < sp; i++) stk[(i - kSpill) * kBlock] = stk[i * kBlock];
@@ -548,6 +611,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         --sp;
         if ((unsigned)n - (unsigned)kRefill - 1u < (unsigned)(kStackMax / kSpill)) {   // rare: bring a block back
             const int nb = n - kRefill;
+            if (!check(sp == 0 && n == stk[0] && bottom_ok(n))) return rtbvh::kEmpty;
             const int *o = ovf_lane() + (nb - 1) * kSpill;
             for (int i = 0; i < kSpill; i++) stk[(1 + i) * kBlock] = o[i];
             stk[0] = nb > 1 ? n - 1 : rtbvh::kEmpty;
@@ -560,7 +624,11 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     // One 4-wide node (rt_bvh.h Node4H, child_planes): slab-test the
     // children, push the far hits, continue with the nearest, park the first
     // leaf reached.
+#if RT_NODE8
+    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w4) {
+#else
     auto visit_q = [&](float4 w0, float4 wx, float4 wy, float4 wz, float4 w4) {
+#endif
 #if RT_PROF
         cnt.trips++;
 #endif
@@ -571,8 +639,12 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         const int top0 = stk[(sp - 1) * kBlock];
         float thi = thi_now();
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
+#if RT_NODE8
+        const ChildPlanes cp = child_planes8(w0, w1, w2, ix, iy, iz, ox, oy, oz, m_x, m_y, m_z);
+#else
         const float4 wa[3] = {wx, wy, wz};
         const ChildPlanes cp = child_planes(w0, wa, ix, iy, iz, ox, oy, oz);
+#endif
         unsigned k[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -657,10 +729,15 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         // index counts the waves of one XCD: blockIdx.x / 8)
         const int hw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x >> 3) * (kBlock / 64) + threadIdx.x / 64));
         const int r0 = p.hot_base + (int)((unsigned)hw & p.hot_mask) * p.hot_stride;
+#if RT_NODE8
+        visit_q(sld4b(p.bvh, r0), sld4b(p.bvh, r0 + 16), sld4b(p.bvh, r0 + 32),
+                sld4b(p.bvh, r0 + rtbvh::kNodeQLinkOff));
+#else
         visit_q(sld4b(p.bvh, r0), near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff), neg_x),
                 near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff + 24), neg_y),
                 near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff + 48), neg_z),
                 sld4b(p.bvh, r0 + rtbvh::kNodeLinkOff));
+#endif
     }
     for (;;) {
         while (node >= 0) {
@@ -670,15 +747,25 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
             // node = the node's byte offset (rt_scene.cpp): five buffer loads
             // at immediate offsets from it; each axis window at the ray's
             // near-first offset (wo_*: 0 or 8 bytes, per lane)
+#if RT_NODE8
+            // node = its byte offset: the 64-B node as four aligned 16-B loads
+            const float4 w0 = bld4(bvh_rs, node, 0), w1 = bld4(bvh_rs, node, 16), w2 = bld4(bvh_rs, node, 32);
+            const float4 w4 = bld4(bvh_rs, node, rtbvh::kNodeQLinkOff);
+#else
             const float4 w0 = bld4(bvh_rs, node, 0), w4 = bld4(bvh_rs, node, rtbvh::kNodeLinkOff);
             const float4 wx = bld4(bvh_rs, node + wo_x, rtbvh::kNodeAxisOff);
             const float4 wy = bld4(bvh_rs, node + wo_y, rtbvh::kNodeAxisOff + 24);
             const float4 wz = bld4(bvh_rs, node + wo_z, rtbvh::kNodeAxisOff + 48);
+#endif
 #if RT_PROF >= 2
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(wz.x) : "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w4.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
+#if RT_NODE8
+            visit_q(w0, w1, w2, w4);
+#else
             visit_q(w0, wx, wy, wz, w4);
+#endif
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
@@ -710,6 +797,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         }
         if (node == rtbvh::kEmpty && leaf == rtbvh::kEmpty) break;
     }
+    if (RT_CHECK) (void)check(stk[0] == rtbvh::kEmpty);
     if (q.closest) {
         if (win >= 0) {
             q.tmax = best;
@@ -1947,27 +2035,29 @@ size_t cold_frame_bytes(int maxf) {
     return maxf == 1 ? sizeof(Cold<1>) : maxf == 5 ? sizeof(Cold<5>) : maxf == 9 ? sizeof(Cold<9>) : sizeof(Cold<17>);
 }
 
+// occupancy of the instantiation that will be launched (the counting one may
+// use more registers than the benched one)
 template <int MAXF, int MODE>
-static int blocks_one(size_t lds_bytes) {
+static int blocks_one(bool count, size_t lds_bytes) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE, false>, kBlock, lds_bytes) !=
-        hipSuccess)
-        return 0;
-    return nb;
+    const hipError_t e =
+        count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE, true>, kBlock, lds_bytes)
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel<MAXF, MODE, false>, kBlock, lds_bytes);
+    return e == hipSuccess ? nb : 0;
 }
 
 template <int MAXF>
-static int blocks_mode(int mode, size_t lds_bytes) {
-    if (mode == MODE_BVH) return blocks_one<MAXF, MODE_BVH>(lds_bytes);
-    if (mode == MODE_SCAN_LDS) return blocks_one<MAXF, MODE_SCAN_LDS>(lds_bytes);
-    return blocks_one<MAXF, MODE_SCAN>(lds_bytes);
+static int blocks_mode(int mode, bool count, size_t lds_bytes) {
+    if (mode == MODE_BVH) return blocks_one<MAXF, MODE_BVH>(count, lds_bytes);
+    if (mode == MODE_SCAN_LDS) return blocks_one<MAXF, MODE_SCAN_LDS>(count, lds_bytes);
+    return blocks_one<MAXF, MODE_SCAN>(count, lds_bytes);
 }
 
-int render_blocks_per_cu(int maxf, int mode, size_t lds_bytes) {
-    if (maxf == 1) return blocks_mode<1>(mode, lds_bytes);
-    if (maxf == 5) return blocks_mode<5>(mode, lds_bytes);
-    if (maxf == 9) return blocks_mode<9>(mode, lds_bytes);
-    return blocks_mode<17>(mode, lds_bytes);
+int render_blocks_per_cu(int maxf, int mode, bool count, size_t lds_bytes) {
+    if (maxf == 1) return blocks_mode<1>(mode, count, lds_bytes);
+    if (maxf == 5) return blocks_mode<5>(mode, count, lds_bytes);
+    if (maxf == 9) return blocks_mode<9>(mode, count, lds_bytes);
+    return blocks_mode<17>(mode, count, lds_bytes);
 }
 
 template <int MAXF, bool COUNT>

@@ -14,7 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "rt_accel.h"
@@ -76,6 +78,8 @@ struct rt_scene {
     long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
     long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
     long long opt_counters = kCounters;  // 1: the counting kernel (rt_stats' rays, events, tests); 0: none
+    long long opt_recursive = 0;       // test hook: 1 forces the recursive instantiation (MAXF by depth) on a
+                                       // scene without reflecting / refracting materials (no last-light skip)
     int last_light_skip_auto = 0;      // Params::last_light_skip when exact for the scene
     double bvh_D = -1.0;               // distance bound the current BVH was padded for
     float4 *d_bvh = nullptr;
@@ -100,6 +104,44 @@ namespace {
 
 const char *kErr[] = {"ok", "invalid argument", "no such HIP device", "HIP runtime error", "out of device memory",
                       "unsupported"};
+
+// Streams made ahead of the scenes by rt_device_init (the first stream of a
+// process costs ~10 ms: its hardware queue), taken by rt_scene_create and
+// given back by rt_scene_destroy.
+std::mutex g_pool_mu;
+std::vector<std::pair<int, hipStream_t>> g_stream_pool;
+
+hipStream_t take_stream(int device) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_stream_pool.size(); i++)
+        if (g_stream_pool[i].first == device) {
+            hipStream_t st = g_stream_pool[i].second;
+            g_stream_pool.erase(g_stream_pool.begin() + (long)i);
+            return st;
+        }
+    return nullptr;
+}
+void give_stream(int device, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_stream_pool.emplace_back(device, st);
+}
+
+// RT_TIMING=1 in the environment: the steps of scene creation and of the
+// first renders on the host clock, to stderr (the one-shot CLI's fixed costs,
+// DESIGN.md §7a)
+struct StepTimer {
+    bool on = std::getenv("RT_TIMING") != nullptr;
+    const char *what;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    explicit StepTimer(const char *w) : what(w) {}
+    void mark(const char *step) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[rt timing] %s %s %.3f ms\n", what, step,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
 
 template <typename T, typename P>
 int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
@@ -132,7 +174,9 @@ size_t mode_lds_bytes(const rt_scene *s, int maxf, int mode, Params &p) {
     const size_t end = mode_region_end(s, mode, p);
     const size_t with = end + (size_t)p.nl * sizeof(LightK);
     p.lights_lds = (int)(end / sizeof(float4));
-    p.lights_in_lds = with <= s->max_lds && render_blocks_per_cu(maxf, mode, with) >= render_blocks_per_cu(maxf, mode, end);
+    const bool cnt = s->opt_counters != 0;
+    p.lights_in_lds =
+        with <= s->max_lds && render_blocks_per_cu(maxf, mode, cnt, with) >= render_blocks_per_cu(maxf, mode, cnt, end);
     return p.lights_in_lds ? with : end;
 }
 
@@ -159,9 +203,11 @@ static unsigned refill_for(const rt_scene *s, const Params &p) {
 }
 
 hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, int mode, hipStream_t st, bool dry) {
+    StepTimer tm(dry ? "prepare" : "launch");
     Params pl = p;
     size_t shm = mode_lds_bytes(s, maxf, mode, pl);
-    int nb = render_blocks_per_cu(maxf, mode, shm);
+    int nb = render_blocks_per_cu(maxf, mode, s->opt_counters != 0, shm);
+    tm.mark("occupancy");
     if (nb < 1) nb = 1;
     long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu - s->opt_reserve;
     long long need = ((long long)p.total + kBlock - 1) / kBlock;
@@ -190,6 +236,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
             r.frames_cap = fbytes;
         }
     }
+    tm.mark("frames");
     pl.frames = slot.d_frames;
     pl.ovf = reinterpret_cast<int *>(static_cast<char *>(slot.d_frames) + cold_bytes);
     s->last_blocks_per_cu = nb;
@@ -201,7 +248,9 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     s->last_lights_in_lds = pl.lights_in_lds;
     s->last_work_parts = 1 << pl.work_shift;
     if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
-    return render_launch(maxf, mode, s->opt_counters != 0, pl, (unsigned)grid, shm, st);
+    const hipError_t e = render_launch(maxf, mode, s->opt_counters != 0, pl, (unsigned)grid, shm, st);
+    tm.mark("kernel launch (enqueue)");
+    return e;
 }
 
 // (Re)build the BVH for distance bound D on the host (rt_accel.cpp) and
@@ -215,9 +264,11 @@ int build_bvh(rt_scene *s, double D) {
     o.threads = (int)s->opt_bvh_threads;
     o.hot_copies = (int)s->opt_hot_copies;
     AccelTree T;
+    StepTimer tm("build_bvh");
     build_accel(s->in, D, o, T);
+    tm.mark("host build");
     bool ok = T.ok;
-    const std::vector<rtbvh::Node4H> &QQ = T.nodes;
+    const std::vector<rtbvh::NodeDev> &QQ = T.nodes;
     const std::vector<float4> &rec = T.rec;
     const std::vector<DirK> &dirk = T.dirk;
     const std::vector<int32_t> &objleaf = T.objleaf;
@@ -284,6 +335,7 @@ int build_bvh(rt_scene *s, double D) {
     s->base.hot_stride = hot ? (int)T.hot_stride : 0;
     s->base.hot_mask = hot ? (unsigned)(T.hot_copies - 1) : 0u;
     s->last_hot_copies = hot ? T.hot_copies : 0;
+    tm.mark("upload");
     s->bvh_ok = ok && rc == RT_OK;
     s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
     s->bvh_depth = s->bvh_ok ? T.depth : 0;
@@ -300,7 +352,7 @@ int build_bvh(rt_scene *s, double D) {
 
 int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = false) {
     int depth = p.depth < 0 ? 0 : p.depth;
-    const int maxf = maxf_for(depth, s->secondary);
+    const int maxf = maxf_for(depth, s->secondary || (s->opt_recursive && depth > 0));
     if (maxf < 0) return RT_E_UNSUPPORTED;
     int nobj = p.nf + p.ns;
     bool bvh = s->opt_accel == 1 || (s->opt_accel == -1 && nobj > 32);
@@ -458,9 +510,11 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     for (int i = 0; i < desc->n_textures; i++)
         if (desc->textures[i].width <= 0 || desc->textures[i].height <= 0 || !desc->textures[i].rgb)
             return RT_E_INVALID;
+    StepTimer tm("rt_scene_create");
     int ndev = rt_device_count();
     if (device < 0 || device >= ndev) return RT_E_NODEVICE;
     if (hipSetDevice(device) != hipSuccess) return RT_E_HIP;
+    tm.mark("device");
 
     auto *s = new rt_scene();
     s->device = device;
@@ -468,6 +522,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
 
     // the per-object arrays and the BVH sources, on the host (rt_accel.cpp)
     accel_input(desc, s->in);
+    tm.mark("host arrays");
     const AccelInput &in = s->in;
     s->secondary = in.secondary;
     std::vector<TexK> texs((size_t)desc->n_textures);
@@ -488,11 +543,16 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     }
     if (!rc) rc = upload(s, texels, p.texels);
     if (!rc) rc = upload(s, texs, p.texs);
-    if (!rc && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) rc = RT_E_HIP;
+    tm.mark("uploads");
+    if (!rc && !(s->stream = take_stream(device)) &&
+        hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = RT_E_HIP;
+    tm.mark("stream");
     if (!rc) {
         s->slots.assign(1, RenderSlot{});
         rc = init_slot(s->slots[0], false);
     }
+    tm.mark("slot");
     if (!rc) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) rc = RT_E_HIP;
@@ -501,6 +561,7 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
             s->max_lds = prop.sharedMemPerBlock;
         }
     }
+    tm.mark("properties");
     if (rc) {
         rt_scene_destroy(s);
         return rc;
@@ -553,9 +614,38 @@ int rt_scene_destroy(rt_scene *s) {
     if (s->dev_out) (void)hipFree(s->dev_out);
     if (s->dev_pix) (void)hipFree(s->dev_pix);
     for (auto &r : s->slots) free_slot(r);
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->stream) give_stream(s->device, s->stream);   // (synchronised above) for the next scene
     delete s;
     return RT_OK;
+}
+
+int rt_device_init(int device) {
+    StepTimer tm("rt_device_init");
+    const int ndev = rt_device_count();
+    if (device < 0 || device >= ndev) return RT_E_NODEVICE;
+    if (hipSetDevice(device) != hipSuccess || hipFree(nullptr) != hipSuccess) return RT_E_HIP;
+    tm.mark("context");
+    // the runtime's lazily made state: device memory, the staging paths of
+    // both copy directions, a hardware queue (a stream kept for the next
+    // rt_scene_create), the kernels' code object (an occupancy query)
+    void *d = nullptr;
+    unsigned char h[4096] = {0};
+    int rc = RT_OK;
+    if (hipMalloc(&d, sizeof h) != hipSuccess) return RT_E_NOMEM;
+    if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = RT_E_HIP;
+    (void)hipFree(d);
+    tm.mark("memory + copies");
+    hipStream_t st = nullptr;
+    if (!rc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+        if (hipStreamSynchronize(st) == hipSuccess) give_stream(device, st);
+        else (void)hipStreamDestroy(st);
+    }
+    tm.mark("stream");
+    (void)render_blocks_per_cu(maxf_for_depth(4), MODE_BVH, false, 32 * 1024);
+    tm.mark("code object");
+    return rc;
 }
 
 int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
@@ -607,6 +697,10 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         if (value < 0 || value > 1) return RT_E_INVALID;
         s->opt_counters = value;
     }
+    else if (k == "recursive") {
+        if (value < 0 || value > 1) return RT_E_INVALID;
+        s->opt_recursive = value;
+    }
     else if (k == "hot_copies") {
         if (value < 0 || value > 64 || (value & (value - 1))) return RT_E_INVALID;
         s->opt_hot_copies = value;
@@ -618,7 +712,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
 
 int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int block, int step,
                                int nrows, float *out_rgb, void *hip_stream) {
-    if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || block < 1 || step < block || nrows < 1)
+    if (!s || !cam || !out_rgb || W < 1 || H < 1 || y0 < 0 || block < 1 || step < block || nrows < 1)
         return RT_E_INVALID;
     long long last = (long long)y0 + (long long)((nrows - 1) / block) * step + (nrows - 1) % block;
     if (last >= H) return RT_E_INVALID;
@@ -636,7 +730,7 @@ int rt_render_row_blocks_async(rt_scene *s, const rt_camera *cam, int W, int H, 
 
 int rt_render_pixels(rt_scene *s, const rt_camera *cam, int W, int H, const int *xy, int n, float *out_rgb,
                      rt_stats *stats) {
-    if (!s || !cam || !xy || !out_rgb || W < 2 || H < 2 || n < 1) return RT_E_INVALID;
+    if (!s || !cam || !xy || !out_rgb || W < 1 || H < 1 || n < 1) return RT_E_INVALID;
     for (int k = 0; k < n; k++)
         if (xy[2 * k] < 0 || xy[2 * k] >= W || xy[2 * k + 1] < 0 || xy[2 * k + 1] >= H) return RT_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
@@ -699,7 +793,7 @@ int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *
 }
 
 int rt_scene_prepare(rt_scene *s, const rt_camera *cam, int W, int H) {
-    if (!s || !cam || W < 2 || H < 2) return RT_E_INVALID;
+    if (!s || !cam || W < 1 || H < 1) return RT_E_INVALID;
     if ((long long)W * H >= (1ll << 31)) return RT_E_UNSUPPORTED;
     if (hipSetDevice(s->device) != hipSuccess) return RT_E_HIP;
     Params p = s->base;
@@ -834,7 +928,7 @@ int rt_scene_debug_wavelog(rt_scene *s, unsigned long long *out, int n) {
 }
 
 int rt_render_rows(rt_scene *s, const rt_camera *cam, int W, int H, int y0, int y1, float *out_rgb, rt_stats *stats) {
-    if (!s || !cam || !out_rgb || W < 2 || H < 2 || y0 < 0 || y1 > H || y0 >= y1) return RT_E_INVALID;
+    if (!s || !cam || !out_rgb || W < 1 || H < 1 || y0 < 0 || y1 > H || y0 >= y1) return RT_E_INVALID;
     return rt_render_row_blocks(s, cam, W, H, y0, y1 - y0, y1 - y0, y1 - y0, out_rgb, stats);
 }
 
@@ -860,13 +954,17 @@ int rt_render_row_blocks(rt_scene *s, const rt_camera *cam, int W, int H, int y0
         }
         dst = s->dev_out;
     }
+    StepTimer tm("rt_render_row_blocks");
     int rc = rt_render_row_blocks_async(s, cam, W, H, y0, block, step, nrows, dst, nullptr);
     if (rc) return rc;
+    tm.mark("submitted");
     if (!on_device && hipMemcpyAsync(out_rgb, dst, bytes, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
         return RT_E_HIP;
     if (hipStreamSynchronize(s->stream) != hipSuccess) return RT_E_HIP;
-    if (stats) return rt_scene_last_stats(s, stats);
-    return RT_OK;
+    tm.mark("synchronized");
+    if (stats) rc = rt_scene_last_stats(s, stats);
+    tm.mark("stats");
+    return rc;
 }
 
 }  // extern "C"

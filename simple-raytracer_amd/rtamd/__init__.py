@@ -86,8 +86,9 @@ _hip = None
 
 HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_set_imsize",
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
-                "rth_output_path", "rth_row_set", "rth_ppm_open", "rth_ppm_write_rows", "rth_ppm_close"]
-HIP_SYMBOLS = ["rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
+                "rth_output_path", "rth_row_set", "rth_ppm_open", "rth_ppm_write_rows", "rth_ppm_close",
+                "rth_write_ppm_u8", "rth_ppm_write_rows_u8"]
+HIP_SYMBOLS = ["rt_device_count", "rt_device_init", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_scene_debug_ub_pixels",
@@ -118,6 +119,9 @@ def host_lib() -> C.CDLL:
             L.rth_ppm_open.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
             L.rth_ppm_write_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
             L.rth_ppm_close.argtypes = [C.c_void_p]
+        if hasattr(L, "rth_write_ppm_u8"):   # absent from round-1..4 libraries (A/B baselines)
+            L.rth_write_ppm_u8.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+            L.rth_ppm_write_rows_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         if hasattr(L, "rth_row_set"):     # absent from round-1 libraries (A/B baselines)
             L.rth_row_set.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4
         _host = L
@@ -141,6 +145,8 @@ def hip_lib() -> C.CDLL:
             pass
         L = C.CDLL(path)
         L.rt_device_count.restype = C.c_int
+        if hasattr(L, "rt_device_init"):        # absent from round-1..4 libraries (A/B baselines)
+            L.rt_device_init.argtypes = [C.c_int]
         L.rt_scene_create.argtypes = [C.c_int, C.POINTER(rt_scene_desc), C.POINTER(C.c_void_p)]
         L.rt_scene_destroy.argtypes = [C.c_void_p]
         L.rt_render_rows.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
@@ -272,6 +278,15 @@ def write_ppm(path: str, rgb: np.ndarray, threads: int = 0) -> None:
         raise RTError(f"cannot write {path}")
 
 
+def write_ppm_u8(path: str, v: np.ndarray, threads: int = 0) -> None:
+    """The P3 file from the pixel values as bytes (rth_write_ppm_u8): the
+    values rt_quantize_u8 makes when all are 0..255."""
+    a = np.ascontiguousarray(v, dtype=np.uint8)
+    H, W = a.shape[:2]
+    if host_lib().rth_write_ppm_u8(os.fsencode(path), a.ctypes.data, W, H, threads) != 0:
+        raise RTError(f"cannot write {path}")
+
+
 def write_ppm_blocks(path: str, rgb: np.ndarray, block: int, threads: int = 0) -> None:
     """The P3 file written in blocks of `block` rows (rth_ppm_open / rth_ppm_write_rows /
     rth_ppm_close): byte-identical to write_ppm."""
@@ -332,6 +347,9 @@ class GpuScene:
             # staging buffer, which may still hold an earlier render)
             import torch
             dev = torch.full((y1 - y0, W, 3), float("nan"), dtype=torch.float32, device=f"cuda:{self.device}")
+            # the fill runs on torch's stream, the render on the scene's own
+            # (non-blocking) stream: nothing orders the two but this wait
+            torch.cuda.synchronize(self.device)
             _check(hip_lib().rt_render_rows(self._h, C.byref(cam), W, H, y0, y1, C.c_void_p(dev.data_ptr()),
                                             C.byref(st)), "rt_render_rows")
             return dev.cpu().numpy(), st

@@ -46,11 +46,14 @@ def test_bvh_device_padding_stack(checker):
 
 
 # Tree hashes (tools/bvh_bench.cpp: FNV-1a over the uploaded node, record,
-# object-leaf and cone-tree arrays) of the seeded benchmark scenes: the
-# round-3 builder's trees.  The round-4 builder (primitive array reordered in
-# place, one-pass range statistics, sparse bins for small ranges, subtrees on
-# threads, bitwise binary16 rounding) must build the same trees.
-BENCH_TREE_HASH = {"C3": "d0d4c36f4057bc62", "C4": "5023c92e900cccd1", "C5": "0fa041b2ecb60269"}
+# object-leaf and cone-tree arrays) of the seeded benchmark scenes, by device
+# node size.  104: the round-3 builder's trees with binary16 nodes (RT_NODE8=0);
+# the round-4 builder (primitive array reordered in place, one-pass range
+# statistics, sparse bins for small ranges, subtrees on threads, bitwise
+# binary16 rounding) builds the same trees.  64: the same trees stored as the
+# round-5 64-B nodes with 8-bit planes (RT_NODE8=1, the default).
+BENCH_TREE_HASH = {104: {"C3": "d0d4c36f4057bc62", "C4": "5023c92e900cccd1", "C5": "0fa041b2ecb60269"},
+                   64: {"C3": "04afc4732a2a9f6b", "C4": "a76af2eedeb8ab63", "C5": "c6ebbeb0f0baad7c"}}
 
 
 @pytest.fixture(scope="module")
@@ -72,7 +75,7 @@ def test_bvh_build_threads_identical(bvh_bench, tmp_path, cfg):
     assert r.returncode == 0, r.stdout + r.stderr
     j = json.loads(r.stdout)
     assert j["identical"] and j["ok"] == 1, j
-    assert j["hash"] == BENCH_TREE_HASH[cfg], j
+    assert j["hash"] == BENCH_TREE_HASH[j["node_bytes"]][cfg], j
     # 16 hot copies of the top (option hot_copies): each copy's walk reads
     # the main tree's bounds and leaf records, the main arrays unchanged
     assert j["hot_ok"] and j["hot_copies"] == 16 and j["hot_per_copy"] == min(64, j["main_nodes"]), j

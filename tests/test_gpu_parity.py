@@ -126,29 +126,65 @@ def test_c5_depth8_mini():
     assert _counts(st) == cnt
 
 
-def test_c3_full_size_row_sample(tmp_path):
-    """BASELINE config C3 at its full 4096x4096: the GPU image is compared
-    with the oracle on a sample of rows (the oracle cannot render all of it in
-    test time); total rays must be consistent with the sampled rays/row."""
-    path = gen.write_scene(str(tmp_path), "C3")
-    img, st = rtamd.render_scene(path)
-    H = img.shape[0]
-    rows = np.linspace(0, H - 1, 12).astype(np.int32)
-    o = OracleScene(path)
-    ref, cnt = o.render(rows=rows)
-    assert_parity(img[rows], ref, "C3 row sample")
-    assert st.primary == 4096 * 4096
-    # the sampled rows' rays, recomputed on the GPU for the same rows
-    hs = rtamd.HostScene(path)
-    gs = rtamd.GpuScene(hs)
+def _benched_rows_vs_oracle(tmp_path, config: str, nrows: int, depth: int = 4, key: str | None = None,
+                            dense_row: bool = False):
+    """A BASELINE config at its full size, rendered whole into HBM by the
+    kernel instantiation bench.py times (option counters = 0), compared on
+    `nrows` rows spread over the image with the oracle; the same rows'
+    pixels rendered again by the counting instantiation (rt_render_pixels)
+    are bit for bit the timed image's, with exactly the oracle's per-type ray
+    counts (main.cpp:718-764)."""
+    torch = pytest.importorskip("torch")
+    d = str(tmp_path)
+    path = gen.write_scene(d, config)
+    hs = rtamd.HostScene(path, cwd=d)
+    hs.set_depth(depth)
+    W, H = hs.width, hs.height
     cam = hs.camera()
-    tot = {k: 0 for k in RAYS}
-    for r in rows:
-        _, s = gs.render_rows(cam, 4096, 4096, int(r), int(r) + 1)
-        for k in RAYS:
-            tot[k] += int(getattr(s, k))
-    assert tot == {k: cnt[k] for k in RAYS}
-    _summary["C3_full_rows"] = dict(compare(img[rows], ref), gpu_total=_counts(st), sample=cnt)
+    gs = rtamd.GpuScene(hs)
+    gs.set_option("counters", 0)
+    img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+    gs.render_rows_async(cam, W, H, 0, H, img.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    gs.last_stats()
+    torch.cuda.synchronize()
+    assert gs.debug_counters()[48] == 0          # the uncounted (benched) instantiation ran
+    rows = np.unique(np.linspace(0, H - 1, nrows).astype(np.int32))
+    if dense_row:
+        rows[0] = H // 3                     # the image's top rows are mostly sky: take a dense one too
+        rows = np.unique(rows)
+    got = img[rows.tolist()].cpu().numpy()
+    del img
+    o = OracleScene(path, cwd=d)
+    o.set_depth(depth)
+    ref, cnt = o.render(rows=rows)
+    c = assert_parity(got, ref, f"{config} rows (counters=0)")
+    gs.set_option("counters", 1)
+    xs, ys = np.meshgrid(np.arange(W, dtype=np.int32), rows)
+    xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
+    alone, st_px = gs.render_pixels(cam, W, H, xy)
+    assert np.array_equal(np.nan_to_num(alone.reshape(got.shape), nan=-9), np.nan_to_num(got, nan=-9))
+    assert _counts(st_px) == cnt, (_counts(st_px), cnt)
+    gs.close()
+    _summary[key or f"{config}_full_rows_counters0"] = dict(c, rows=len(rows), pixels=int(len(xy)), sample=cnt)
+    return c, cnt
+
+
+def test_c3_full_size_row_sample(tmp_path):
+    """BASELINE config C3 at its full 4096x4096 (the bench's workload), by the
+    benched instantiation: 256 rows (1 M pixels, ~7 M rays) against the
+    oracle, exact per-type counts of those rows."""
+    _, cnt = _benched_rows_vs_oracle(tmp_path, "C3", 256, key="C3_full_rows")
+    assert cnt["refraction"] > 0 and cnt["reflection"] > 0
+
+
+@pytest.mark.parametrize("config", ["C3G", "C3D"])
+def test_c3_variants_full_size_row_sample(tmp_path, config):
+    """C3G (glass triangles: SKIP_TRANS, main.cpp:1000-1002) and C3D (an
+    unnormalised directional light against spheres, main.cpp:895) at
+    4096x4096 by the benched instantiation: 64 rows against the oracle."""
+    _, cnt = _benched_rows_vs_oracle(tmp_path, config, 64, key=f"{config}_full_rows")
+    if config == "C3G":
+        assert cnt["skip_trans"] > 0
 
 
 def _render_on_device(path: str, cwd: str, depth: int):
@@ -170,26 +206,11 @@ def _render_on_device(path: str, cwd: str, depth: int):
 def test_c4_full_size_row_sample(tmp_path):
     """BASELINE config C4 at its full 8192x8192: 10 000 textured triangles with
     the real-size 2048x1024 synthetic texture, a directional and a point light
-    (hard shadows).  Rows sampled across the image against the oracle, with
-    exact per-row ray counts (main.cpp:718-764)."""
-    d = str(tmp_path)
-    path = gen.write_scene(d, "C4")
-    img, st, hs, gs, cam = _render_on_device(path, d, 4)
-    W, H = hs.width, hs.height
-    assert (W, H) == (8192, 8192) and st.primary == W * H
-    rows = np.linspace(0, H - 1, 6).astype(np.int32)
-    rows[0] = H // 3                      # the image's top rows are mostly sky: take a dense one too
-    got = img[rows.tolist()].cpu().numpy()
-    ref, cnt = OracleScene(path, cwd=d).render(rows=rows)
-    c = assert_parity(got, ref, "C4 row sample")
-    tot = {k: 0 for k in RAYS}
-    for r in rows:
-        _, s = gs.render_rows(cam, W, H, int(r), int(r) + 1)
-        for k in RAYS:
-            tot[k] += int(getattr(s, k))
-    assert tot == {k: cnt[k] for k in RAYS}
+    (hard shadows).  Rendered by the benched instantiation (counters = 0); 8
+    rows across the image (one of them dense) against the oracle, with exact
+    per-type ray counts of those rows (main.cpp:718-764)."""
+    _, cnt = _benched_rows_vs_oracle(tmp_path, "C4", 8, key="C4_full_rows", dense_row=True)
     assert cnt["shadow"] > 0
-    _summary["C4_full_rows"] = dict(c, rows=rows.tolist(), gpu_total=_counts(st), sample=cnt)
 
 
 def test_c5_full_size_span_sample(tmp_path):
@@ -385,7 +406,7 @@ def test_prepare_then_render():
     assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9))
     assert _counts(st2) == _counts(st)
     with pytest.raises(rtamd.RTError):
-        gs.prepare(cam, 1, H)
+        gs.prepare(cam, 0, H)                 # (1 x H is a valid image: the seam's NaN camera)
 
 
 @pytest.mark.parametrize("inflight", [2, 3])
@@ -439,7 +460,7 @@ def test_abi_errors():
     st = rtamd.rt_stats()
     assert L.rt_render_rows(gs._h, C.byref(cam), 64, 64, 5, 5, C.c_void_p(buf.ctypes.data), C.byref(st)) == -1
     assert L.rt_render_rows(gs._h, C.byref(cam), 64, 64, 60, 65, C.c_void_p(buf.ctypes.data), C.byref(st)) == -1
-    assert L.rt_render_rows(gs._h, C.byref(cam), 1, 64, 0, 1, C.c_void_p(buf.ctypes.data), C.byref(st)) == -1
+    assert L.rt_render_rows(gs._h, C.byref(cam), 0, 64, 0, 1, C.c_void_p(buf.ctypes.data), C.byref(st)) == -1
     hs.set_depth(40)
     with pytest.raises(rtamd.RTError):
         g2 = rtamd.GpuScene(hs)
@@ -633,6 +654,97 @@ def _deep_scene_text(w: int = 32, h: int = 32) -> str:
     return "".join(out)
 
 
+_CHECK_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import rtamd
+out = {}
+for name, cwd, depth, opts in json.loads(sys.argv[2]):
+    hs = rtamd.HostScene(name, cwd=cwd)
+    hs.set_depth(depth)
+    W, H = hs.width, hs.height
+    gs = rtamd.GpuScene(hs)
+    for k, v in opts.items():
+        gs.set_option(k, v)
+    img, st = gs.render_rows(hs.camera(), W, H, 0, H)
+    dbg = gs.debug_counters()
+    key = name + json.dumps(opts, sort_keys=True)
+    np.save(os.path.join(sys.argv[3], str(len(out)) + ".npy"), img)
+    out[key] = dict(violations=int(dbg[49]), spills=int(st.stack_spills), rays=st.rays(), idx=len(out))
+    gs.close()
+print(json.dumps(out))
+"""
+
+
+def test_rt_check_stack_bottom_invariant(tmp_path):
+    """The RT_CHECK build (simple-raytracer_amd/lib_check/, never benched)
+    checks the BVH stack-bottom invariant -- entry 0 is kEmpty or a refill
+    tag kRefill + b with b spilled blocks inside the lane's spill area -- at
+    every traversal entry and exit, spill and refill (rt_kernels.hip
+    bvh_trace; round 4's suspended-search variant faulted by breaking it).
+    On the scenes that spill most (the skewed deep tree and C3 / C5 with a
+    12-entry LDS share) no violation is counted, and the images and ray
+    counts equal the benched library's bit for bit."""
+    lib = os.path.join(PKG, "lib_check", "librt_hip.so")
+    if not os.path.exists(lib):
+        pytest.fail("lib_check/ missing: __graft_entry__.build() (make -C simple-raytracer_amd check)")
+    (tmp_path / "deep.txt").write_text(_deep_scene_text())
+    cases = [("deep.txt", str(tmp_path), 4, {}), ("deep.txt", str(tmp_path), 4, {"lds_stack": 12}),
+             ("C3_64x64.txt", SCENES, 4, {"lds_stack": 12}), ("C5_8x8.txt", SCENES, 8, {"lds_stack": 12}),
+             ("C5_8x8.txt", SCENES, 8, {})]
+    env = dict(os.environ, RTAMD_LIB_DIR=os.path.join(PKG, "lib_check"))
+    r = subprocess.run([sys.executable, "-c", _CHECK_SCRIPT, PKG, json.dumps(cases), str(tmp_path)],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    spills = 0
+    for name, cwd, depth, opts in cases:
+        key = name + json.dumps(opts, sort_keys=True)
+        g = got[key]
+        assert g["violations"] == 0, (key, g)
+        spills += g["spills"]
+        hs = rtamd.HostScene(name, cwd=cwd)
+        hs.set_depth(depth)
+        gs = rtamd.GpuScene(hs)
+        for k, v in opts.items():
+            gs.set_option(k, v)
+        ref, st = gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
+        img = np.load(str(tmp_path / f"{g['idx']}.npy"))
+        assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), key
+        assert g["rays"] == st.rays() and g["spills"] == st.stack_spills, (key, g, st.rays())
+        gs.close()
+    assert spills > 0
+    _summary["rt_check"] = got
+
+
+@pytest.mark.parametrize("size", [(1, 7), (7, 1), (1, 1)])
+def test_degenerate_image_sizes(size):
+    """The seam (main.cpp:670) takes any image size: for a 1-pixel-wide or
+    -tall image its camera deltas divide by res - 1 = 0 (main.cpp:709-710),
+    every primary ray is NaN and meets nothing, and the image is the
+    background.  rt_render_rows does the same, against the oracle's camera
+    and render at that size, with identical ray counts.  (The reference's
+    parser rejects such an imsize, main.cpp:242; test_host.py checks the CLI
+    does too.)"""
+    W, H = size
+    for name in ("test7_s.txt", "C3_64x64.txt"):
+        hs = rtamd.HostScene(name, cwd=SCENES)
+        cam = hs.camera(W, H)
+        gs = rtamd.GpuScene(hs)
+        img, st = gs.render_rows(cam, W, H, 0, H)
+        px, _ = gs.render_pixels(cam, W, H, np.array([[W - 1, H - 1]], dtype=np.int32))
+        gs.close()
+        ref, cnt = OracleScene(name, cwd=SCENES).render(W, H)
+        assert_parity(img, ref, f"{name} {W}x{H}")
+        assert _counts(st) == cnt
+        assert st.primary == W * H
+        bkg = OracleScene(name, cwd=SCENES).globals()[:3]
+        if W == 1 or H == 1:
+            assert np.array_equal(img.reshape(-1, 3), np.broadcast_to(bkg, (W * H, 3))), img
+        assert np.array_equal(px[0], img[H - 1, W - 1])
+
+
 def test_nan_rays_on_the_bvh():
     """Rays with a NaN origin or direction (test7's and Test1's eta = 0
     materials produce them) meet nothing in the reference; the
@@ -724,6 +836,42 @@ def test_refill_options_bit_identical():
     for bad in ({"chunk": -1}, {"refill_min": 0}, {"refill_min": 65}, {"gate_x": 65}):
         with pytest.raises(rtamd.RTError):
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
+
+
+def test_last_light_skip_and_recursive_instantiation_bit_identical():
+    """Scenes without reflecting or refracting materials render with the
+    MAXF = 1 instantiation, which counts a last light's shadow ray whose Phong
+    term is exactly 0 without searching it (option last_light_skip; exact:
+    its contribution is light colour x mask x 0 whatever the mask).  With the
+    skip off, and with the recursive instantiation forced (option recursive,
+    which has no skip), on scenes with four lights and back-facing triangles
+    (never flipped, main.cpp:869-872): the same image and per-type ray counts
+    bit for bit, equal to the oracle's; the skip did fire."""
+    extra = "light 5 20 -30 1 0.4 0.3 0.2\nlight -15 -5 -10 1 0.3 0.3 0.5\n"
+    fired = 0
+    for base in ("C4_32x32.txt", "C2_128x128.txt"):
+        name = "_lls_" + base
+        p = os.path.join(SCENES, name)
+        open(p, "w").write(open(os.path.join(SCENES, base)).read() + extra)
+        try:
+            ref, st = rtamd.render_scene(name, cwd=SCENES)
+            oi, o_cnt = OracleScene(name, cwd=SCENES).render()
+            assert_parity(ref, oi, f"{name} default")
+            assert _counts(st) == o_cnt
+            for opts in ({"last_light_skip": 0}, {"recursive": 1}, {"recursive": 1, "counters": 0},
+                         {"last_light_skip": 0, "counters": 0}):
+                img, st2 = rtamd.render_scene(name, cwd=SCENES, options=opts)
+                assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, opts)
+                if opts.get("counters", 1):
+                    assert _counts(st2) == _counts(st), (name, opts)
+                    if opts.get("last_light_skip", 1) == 0 or opts.get("recursive"):
+                        fired += int(st.shadow_known - st2.shadow_known)
+                        assert st2.shadow_known <= st.shadow_known
+        finally:
+            os.remove(p)
+    assert fired > 0
+    with pytest.raises(rtamd.RTError):
+        rtamd.render_scene("test7_s.txt", cwd=SCENES, options={"recursive": 2})
 
 
 def test_work_bands_hot_copies_counters_bit_identical():
@@ -957,28 +1105,38 @@ def test_deinterleave_rows_device():
 
 @pytest.mark.parametrize("block", ["100000", "1", "7", "64"])
 def test_cli_streamed_ppm_matches(block, tmp_path):
-    """Without --float-out the one-device CLI copies the image to the host in
-    row blocks through pinned buffers and writes each while the next copies
-    (stream_ppm, rth_ppm_*; images of 512 MB and more, or whenever
-    RT_PPM_BLOCK_ROWS is set): the P3 file is byte-identical to the one
-    written from the whole float image (--float-out takes that path), for one
-    block and for 1-, 7- and 64-row blocks on a ragged image."""
-    name = "test7_s.txt"
-    outs = []
-    for args, env in ((["--float-out", str(tmp_path / "f.bin")], {}), ([], {"RT_PPM_BLOCK_ROWS": block})):
-        tmp_name = "_stream_" + name
-        shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
-        out = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
-        try:
-            r = subprocess.run([CLI, tmp_name] + args, cwd=SCENES, capture_output=True, text=True, timeout=300,
-                               env={**os.environ, **env})
-            assert r.returncode == 0, r.stderr
-            outs.append(open(out, "rb").read())
-        finally:
-            for p in (os.path.join(SCENES, tmp_name), out):
-                if os.path.exists(p):
-                    os.remove(p)
-    assert outs[0] == outs[1] and len(outs[0]) > 1000
+    """Without --float-out the one-device CLI quantises the image on the
+    device and copies 3 bytes per pixel to the host in row blocks, each block
+    formatted as soon as it lands (write_ppm_bytes, rth_ppm_write_rows_u8);
+    when some value is not 0..255 (test7: NaN pixels) it falls back to the
+    floats, copied in row blocks through pinned buffers and written while the
+    next block copies (stream_ppm; images of 512 MB and more, or whenever
+    RT_PPM_BLOCK_ROWS is set; RT_PPM_FLOATS forces the floats).  Every way
+    writes the P3 file byte for byte as the one written from the whole float
+    image (--float-out takes that path), for one block and for 1-, 7- and
+    64-row blocks on ragged images."""
+    import json as _json
+    for name, want_from in (("test7_s.txt", "floats"), ("C3_64x64.txt", "bytes")):
+        outs, froms = [], []
+        modes = [(["--float-out", str(tmp_path / "f.bin")], {}), ([], {"RT_PPM_BLOCK_ROWS": block}),
+                 ([], {"RT_PPM_BLOCK_ROWS": block, "RT_PPM_FLOATS": "1"}), ([], {})]
+        for args, env in modes:
+            tmp_name = "_stream_" + name
+            shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
+            out = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
+            sj = str(tmp_path / "stats.json")
+            try:
+                r = subprocess.run([CLI, tmp_name, "--stats-json", sj] + args, cwd=SCENES, capture_output=True,
+                                   text=True, timeout=300, env={**os.environ, **env})
+                assert r.returncode == 0, r.stderr
+                outs.append(open(out, "rb").read())
+                froms.append(_json.load(open(sj))["ppm_from"])
+            finally:
+                for p in (os.path.join(SCENES, tmp_name), out):
+                    if os.path.exists(p):
+                        os.remove(p)
+        assert len(outs[0]) > 1000 and all(o == outs[0] for o in outs), (name, [len(o) for o in outs])
+        assert froms == ["floats", want_from, "floats", want_from], (name, froms)
 
 
 @pytest.mark.parametrize("name", ["test7_s.txt", "C3_64x64.txt"])

@@ -66,7 +66,9 @@ def test_parser_matches_oracle(name):
 def test_camera_matches_oracle(name):
     hs = rtamd.HostScene(name, cwd=SCENES)
     os_ = OracleScene(name, cwd=SCENES)
-    for W, H in [(hs.width, hs.height), (37, 23)]:
+    # (1, 7), (7, 1), (1, 1): the seam's division by res - 1 = 0
+    # (main.cpp:709-710) -- inf / NaN deltas, equal NaN for NaN
+    for W, H in [(hs.width, hs.height), (37, 23), (1, 7), (7, 1), (1, 1)]:
         cam = hs.camera(W, H)
         mine = np.array([*cam.eye, *cam.ul, *cam.dh, *cam.dv], np.float32)
         np.testing.assert_array_equal(mine, os_.camera(W, H))
@@ -88,6 +90,35 @@ def test_quantize_and_writer_match_reference_format():
         assert open(p, "rb").read() == ppm_bytes(img)
     # NaN prints as the reference's size_t(INT_MIN)
     assert b"18446744071562067968" in ppm_bytes(img)
+
+
+def test_byte_writer_matches_float_writer():
+    """rth_write_ppm_u8 / rth_ppm_write_rows_u8 (the CLI's 3-byte path: the
+    device quantises, the host formats bytes) write the float writer's file
+    byte for byte whenever every value is 0..255 -- including the level
+    boundaries 0 and 255 (1.0 * 255 = 255)."""
+    import tempfile
+    rng = np.random.default_rng(11)
+    img = rng.uniform(0, 1, size=(123, 77, 3)).astype(np.float32)
+    img[0, 0] = [0.0, 1.0, np.nextafter(np.float32(1.0), np.float32(0))]
+    img[1, 1] = [1 / 255, 254.99998 / 255, 0.5]
+    q = rtamd.quantize(img)
+    assert q.min() >= 0 and q.max() <= 255
+    v = q.astype(np.uint8)
+    with tempfile.TemporaryDirectory() as td:
+        a, b = os.path.join(td, "a.ppm"), os.path.join(td, "b.ppm")
+        rtamd.write_ppm(a, img, threads=4)
+        rtamd.write_ppm_u8(b, v, threads=3)
+        assert open(a, "rb").read() == open(b, "rb").read() == ppm_bytes(img)
+        L = rtamd.host_lib()
+        import ctypes as C
+        h = C.c_void_p()
+        assert L.rth_ppm_open(os.fsencode(b), 77, 123, 2, C.byref(h)) == 0
+        for y in range(0, 123, 50):
+            n = min(50, 123 - y)
+            assert L.rth_ppm_write_rows_u8(h, v[y:y + n].ctypes.data, n) == 0
+        assert L.rth_ppm_close(h) == 0
+        assert open(b, "rb").read() == ppm_bytes(img)
 
 
 def test_writer_large_parallel_matches():
@@ -209,7 +240,12 @@ REF_ERROR_SCENES = {
     "sphere_before_mtlcolor": BASE + "sphere 0 0 -3 1\n",
     "mtlcolor_3_args": BASE + "mtlcolor 1 1 1\n",
     "hfov_not_a_number": BASE.replace("hfov 60", "hfov abc"),
+    # a 1-pixel-wide or -tall image: the reference's parser rejects it
+    # (main.cpp:242) before the seam's division by res - 1 = 0 is reached
     "imsize_width_1": BASE.replace("imsize 8 8", "imsize 1 8"),
+    "imsize_1_7": BASE.replace("imsize 8 8", "imsize 1 7"),
+    "imsize_7_1": BASE.replace("imsize 8 8", "imsize 7 1"),
+    "imsize_1_1": BASE.replace("imsize 8 8", "imsize 1 1"),
     "light_3_args": BASE + "light 1 1 1\n",
     **{f"missing_{k}": "\n".join(l for l in BASE.splitlines() if not l.startswith(k + " ")) + "\n"
        for k in ("imsize", "eye", "viewdir", "updir", "hfov", "bkgcolor")},

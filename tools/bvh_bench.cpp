@@ -55,8 +55,8 @@ struct Walk {
         const unsigned char *b = static_cast<const unsigned char *>(p);
         for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
     }
-    const rtbvh::Node4H *node(int32_t link) {
-        const size_t nb = sizeof(rtbvh::Node4H), off = (size_t)link;
+    const rtbvh::NodeDev *node(int32_t link) {
+        const size_t nb = sizeof(rtbvh::NodeDev), off = (size_t)link;
         if (t.hot_copies > 1 && off >= t.hot_base) {
             const size_t c = (off - t.hot_base) / t.hot_stride, r = (off - t.hot_base) % t.hot_stride;
             if (c >= (size_t)t.hot_copies || r % nb || r / nb >= (size_t)t.hot_per_copy) return nullptr;
@@ -77,15 +77,15 @@ struct Walk {
             mix(&t.rec[(size_t)off], words * sizeof(t.rec[0]));
             return;
         }
-        const rtbvh::Node4H *z = node(link);
+        const rtbvh::NodeDev *z = node(link);
         if (!z) { bad = true; return; }
-        mix(z, rtbvh::kNodeLinkOff);
+        mix(z, rtbvh::kNodeDevLinkOff);
         for (int32_t l : z->link) go(l, depth + 1);
     }
 };
 
 static bool hot_ok(const AccelTree &ref, const AccelTree &hot, int K, unsigned long long &walk_hash) {
-    const size_t nb = sizeof(rtbvh::Node4H);
+    const size_t nb = sizeof(rtbvh::NodeDev);
     if (!hot.ok || hot.hot_copies != K || hot.nodes.size() != ref.nodes.size() ||
         std::memcmp(hot.nodes.data(), ref.nodes.data(), ref.nodes.size() * nb) != 0 ||
         hot.rec.size() < ref.rec.size() ||
@@ -166,10 +166,11 @@ int main(int argc, char **argv) {
                 "\"input_ms\": %.3f, \"nodes\": %zu, \"main_nodes\": %lld, \"ok\": %d, \"threads\": %d, "
                 "\"serial_ms\": %.3f, \"threaded_ms\": %.3f, \"serial_phases_ms\": %s, \"threaded_phases_ms\": %s, "
                 "\"identical\": %s, \"hash\": \"%016llx\", \"hot_copies\": %d, \"hot_per_copy\": %d, "
-                "\"hot_records\": %zu, \"hot_ok\": %s, \"walk_hash\": \"%016llx\"}\n",
+                "\"hot_records\": %zu, \"hot_ok\": %s, \"walk_hash\": \"%016llx\", \"node_bytes\": %zu}\n",
                 argv[1], in.nf, in.ns, (int)in.lights.size(), parse_ms, input_ms, ref.nodes.size(), ref.main_nodes,
                 ref.ok ? 1 : 0, par.threads, best[0], best[1], phases(0), phases(1), ident ? "true" : "false", tree_hash(ref),
-                hot.hot_copies, hot.hot_per_copy, hot.rec.size() - ref.rec.size(), hot_good ? "true" : "false", walk);
+                hot.hot_copies, hot.hot_per_copy, hot.rec.size() - ref.rec.size(), hot_good ? "true" : "false", walk,
+                sizeof(rtbvh::NodeDev));
     rth_free(hs);
     return ident && hot_good ? 0 : 3;
 }

@@ -36,13 +36,17 @@ def main():
         js = os.path.join(d, "stats.json")
         cmd = [cli, path, "--depth", str(gen.CONFIGS[cfg]["depth"]), "--stats-json", js]
         t0 = time.perf_counter()
-        r = subprocess.run(cmd, cwd=d, capture_output=True, text=True, timeout=600)
+        # RT_TIMING: the library's own step times (scene creation, BVH upload,
+        # first launch) on stderr, kept in the record
+        r = subprocess.run(cmd, cwd=d, capture_output=True, text=True, timeout=600,
+                           env={**os.environ, "RT_TIMING": "1"})
         wall = time.perf_counter() - t0
         if r.returncode != 0:
             print(f"{cfg}: rt failed rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}", flush=True)
             sys.exit(1)
         j = json.load(open(js))
         j["config"] = cfg
+        j["rt_timing"] = [l[len("[rt timing] "):] for l in r.stderr.splitlines() if l.startswith("[rt timing] ")]
         j["process_wall_ms"] = round(wall * 1e3, 1)
         j["note"] = ("phases on the host clock inside one `rt scene.txt` run (N=1); process_wall_ms adds process "
                      "start, HIP runtime initialisation and exit")

@@ -105,6 +105,50 @@ def main():
     bpp = 4 if int(flag.item()) else 1
     out["gather_format"] = "f32" if bpp == 4 else "u8"
     del whole, q8
+
+    # Rank 0's per-frame work beyond its render at N > 1 (bench.py step():
+    # every rank quantises its strip, rt_quantize_u8; rank 0 then launches the
+    # gather and puts N gathered strips in image order with N index_copy_),
+    # measured on this GPU with the buffers of an N-rank run; the collective's
+    # launch by a one-rank NCCL gather of the strip (its data path, xGMI, is
+    # the estimate below)
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from rtamd.dist import image_rows
+
+    def timed(fn, reps=30):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / reps
+
+    def rank0_extra(n):
+        fmt = out["gather_format"]
+        per = row_set(H, n, 0)[4]
+        strip = torch.zeros((per, W, 3), dtype=torch.float32, device="cuda")
+        send = torch.zeros((per, W, 3), dtype=torch.uint8 if fmt == "u8" else torch.float32, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        targets = [torch.zeros_like(send) for _ in range(n)]
+        image = torch.empty((H, W, 3), dtype=send.dtype, device="cuda")
+        idx = [torch.tensor(image_rows(H, n, r), dtype=torch.long, device="cuda") for r in range(n)]
+        q_ms = timed(lambda: quantize_u8_device(rtamd, torch, strip, send, flag)) if fmt == "u8" else 0.0
+
+        def scatter():
+            for r in range(n):
+                if idx[r].numel():
+                    image.index_copy_(0, idx[r], targets[r][: idx[r].numel()])
+        copy_ms = timed(scatter)
+        one = [torch.zeros_like(send)]
+        launch_ms = timed(lambda: dist.gather(send, one, dst=0))
+        del strip, send, targets, image
+        return dict(quantise_ms=round(q_ms, 4), index_copy_ms=round(copy_ms, 4),
+                    gather_launch_ms=round(launch_ms, 4), total_ms=round(q_ms + copy_ms + launch_ms, 4))
+
     base = None
     for n in (int(v) for v in a.ns.split(",")):
         ranks = []
@@ -124,10 +168,14 @@ def main():
         p = [x["pipelined_ms"] for x in ranks]
         strip_bytes = row_set(H, n, 0)[4] * W * 3 * bpp
         gather_ms = strip_bytes / (XGMI_GBPS * 1e9) * 1e3 if n > 1 else 0.0
-        step_ms = max(p) + gather_ms           # the gather of frame k overlaps frame k+1 only partly: counted whole
+        # rank 0's extra work (quantise, index_copy_ x N, the gather's launch)
+        # counted whole, like the gather: it overlaps the next frames' renders
+        # only partly
+        extra = rank0_extra(n) if n > 1 else dict(total_ms=0.0)
+        step_ms = max(p) + gather_ms + extra["total_ms"]
         ent = dict(ranks=ranks, kernel_ms_max=max(k), kernel_ms_mean=round(sum(k) / n, 3),
                    balance=round(sum(k) / n / max(k), 3), pipelined_ms_max=max(p),
-                   gather_ms_est=round(gather_ms, 3), projected_step_ms=round(step_ms, 3),
+                   gather_ms_est=round(gather_ms, 3), rank0_extra=extra, projected_step_ms=round(step_ms, 3),
                    projected_Mrays_per_s=round(rays / step_ms / 1e3, 1))
         if base is None:
             base = ent["projected_Mrays_per_s"]
@@ -135,6 +183,7 @@ def main():
         out["n"][n] = ent
         print(n, {kk: v for kk, v in ent.items() if kk != "ranks"}, flush=True)
     print(json.dumps(out))
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":
