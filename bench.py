@@ -123,7 +123,7 @@ def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
             "sample": f"{config} scene at {sample}x{sample}, oracle restatement, {dt:.1f} s"}
 
 
-def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0) -> dict:
+def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0, threads: int | None = None) -> dict:
     """SURVEY.md §8d's CPU path: this repo's C restatement of the reference
     (oracle/rt_oracle.c: the same brute-force TraceRay/ShadeRay), OpenMP over
     rows on every core this process may run on (its affinity: all the node's
@@ -136,7 +136,7 @@ def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_py import OracleScene
     host = host_cores()
-    threads = host["affinity"]
+    threads = threads or host["affinity"]
 
     def run(side: int):
         d = tempfile.mkdtemp(prefix="rtamd_port_")
@@ -157,20 +157,30 @@ def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0) -> dict:
         side = sample
     return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port", "host": host,
             "sample": f"{config} scene at {side}x{side} (full field of view), {r} rays, {dt:.1f} s, "
-                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows on {threads} threads "
-                      f"(the process's affinity)"}
+                      f"C restatement (oracle/rt_oracle.c), OpenMP over rows on {threads} threads"
+                      + (" (the process's affinity)" if threads == host["affinity"] else "")}
 
 
 def host_cores() -> dict:
     """What the CPU legs may use: the machine's CPUs (nproc of the node), the
-    ones this process may run on (its affinity: a GPU lease's share), and
-    OMP_NUM_THREADS (0 when unset)."""
+    ones this process may run on (its affinity), OMP_NUM_THREADS (0 when
+    unset) and the cgroup's CPU quota in CPUs (cpu.max; None when unlimited or
+    unreadable) -- a GPU lease can see every CPU of the node yet get the time
+    of only a share of them."""
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"nproc": os.cpu_count(), "affinity": aff,
-            "omp_num_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or 0)}
+            "omp_num_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or 0), "cgroup_cpus": quota}
 
 
 def lib_sha16() -> str:
@@ -427,7 +437,18 @@ def main() -> None:
             except Exception as e:  # never lose the GPU line to the CPU leg
                 cpu = {"error": repr(e)}
             try:
+                # every core the process may run on (its affinity) -- and, when
+                # the lease's OMP_NUM_THREADS share is smaller, that share too:
+                # a lease whose cgroup gives it the time of only some of the CPUs
+                # it sees runs the oversubscribed affinity count slower
                 cpu_port = cpu_port_baseline(args.config, 2 * args.cpu_sample)
+                h = cpu_port["host"]
+                share = h["omp_num_threads"] or (int(h["cgroup_cpus"]) if h["cgroup_cpus"] else 0)
+                if 0 < share < h["affinity"]:
+                    cpu_port["at_lease_share"] = cpu_port_baseline(args.config, 2 * args.cpu_sample,
+                                                                   threads=share)
+                    cpu_port["note"] = ("value/cores: all affinity CPUs; at_lease_share: the lease's "
+                                        "OMP_NUM_THREADS share (faster when the cgroup quota is that share)")
             except Exception as e:
                 cpu_port = {"error": repr(e)}
         line = {

@@ -205,6 +205,11 @@ int rt_render_pixels(rt_scene *scene, const rt_camera *cam, int W, int H, const 
  * current device; asynchronous on hip_stream. */
 int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
                          void *hip_stream);
+/* The same for the writer's values as bytes (rt_quantize_u8 output, 3 per
+ * pixel): one kernel puts a byte gather of N ranks in image order (bench.py
+ * rank 0 at N > 1, instead of N index copies). */
+int rt_deinterleave_rows_u8(const unsigned char *gathered, int world, int rows_per, int W, int H, int block,
+                            unsigned char *image, void *hip_stream);
 
 /* The P3 writer's pixel values (main.cpp:760, rth_quantize) of n floats as
  * bytes, on the device: out[i] = (int)(rgb[i] * 255) when that is 0..255;

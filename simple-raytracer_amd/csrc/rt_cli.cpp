@@ -17,9 +17,7 @@
 // the host clock: parse, scene upload, BVH build, render, device->host copy,
 // quantise + P3 write; '-' = stderr).
 #include <chrono>
-#include <condition_variable>
 #include <cstdio>
-#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
@@ -107,13 +105,16 @@ int stream_ppm(const char *path, const float *dimg, int W, int H, int &hip_rc) {
 }
 
 // One device, P3 out from the writer's pixel values as bytes: the device
-// quantises the image (rt_quantize_u8, exact for values 0..255), row blocks
-// of ~16 MB of bytes come to the host on a copier thread, and the writer
-// formats each block (rth_ppm_write_rows_u8) as soon as it has landed --
-// 3 bytes per pixel cross PCIe instead of 12, and the copy hides behind the
-// writer.  Returns 1 when some value is not 0..255 (NaN, a background above
-// 1: the floats must be written, nothing was written), else 0 on success or
-// -1 on a write error; a HIP error goes to hip_rc.  d2h_ms: the copier's time.
+// quantises the image (rt_quantize_u8, exact for values 0..255), 3 bytes per
+// pixel cross PCIe instead of 12 (C3: 50 MB instead of 201 MB, ~5 ms instead
+// of ~19 through pageable memory), and the writer formats the bytes
+// (rth_ppm_write_rows_u8, in row blocks of RT_PPM_BLOCK_ROWS when set: a
+// test hook).  Returns 1 when some value is not 0..255 (NaN, a background
+// above 1: the floats must be written, nothing was written), else 0 on
+// success or -1 on a write error; a HIP error goes to hip_rc.  d2h_ms: the
+// copy's time.  (A copier thread overlapping the copy with the writer was
+// slower on C3 and C5, profiles/r05/e2e_s2*.txt: the pageable copy's
+// staging competes with the writer's threads for the lease's cores.)
 int write_ppm_bytes(const char *path, const float *dimg, int W, int H, int &hip_rc, double &d2h_ms) {
     const size_t n = (size_t)W * H * 3, row = (size_t)W * 3;
     unsigned char *d8 = nullptr;
@@ -129,40 +130,15 @@ int write_ppm_bytes(const char *path, const float *dimg, int W, int H, int &hip_
     if (!hip_rc && (flag & 1u)) ret = 1;
     if (!hip_rc && ret == 0) {
         std::unique_ptr<unsigned char[]> host(new unsigned char[n]);
-        int R = (int)std::max<size_t>(1, std::min<size_t>((size_t)H, (size_t(16) << 20) / std::max<size_t>(1, row)));
-        if (const char *e = std::getenv("RT_PPM_BLOCK_ROWS")) R = std::max(1, std::min(H, std::atoi(e)));   // test hook
-        const int nb = (H + R - 1) / R;
-        std::mutex mu;
-        std::condition_variable cv;
-        int landed = 0;                    // blocks [0, landed) are on the host
-        bool failed = false;
         const auto t0 = Clock::now();
-        std::thread copier([&] {
-            for (int b = 0; b < nb; b++) {
-                const size_t r0 = (size_t)b * R, rows = std::min<size_t>(R, H - r0);
-                const bool ok = hipMemcpy(host.get() + r0 * row, d8 + r0 * row, rows * row, hipMemcpyDeviceToHost) ==
-                                hipSuccess;
-                std::lock_guard<std::mutex> lk(mu);
-                if (!ok) failed = true;
-                landed = ok ? b + 1 : nb;
-                cv.notify_all();
-                if (!ok) break;
-            }
-            d2h_ms = ms_since(t0);
-        });
+        if (hipMemcpy(host.get(), d8, n, hipMemcpyDeviceToHost) != hipSuccess) hip_rc = RT_E_HIP;
+        d2h_ms = ms_since(t0);
+        int R = H;
+        if (const char *e = std::getenv("RT_PPM_BLOCK_ROWS")) R = std::max(1, std::min(H, std::atoi(e)));   // test hook
         rth_ppm_stream *ps = nullptr;
-        bool good = rth_ppm_open(path, W, H, 0, &ps) == 0;
-        for (int b = 0; b < nb; b++) {
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return landed > b; });
-                if (failed) break;
-            }
-            const int rows = std::min(R, H - b * R);
-            if (good && rth_ppm_write_rows_u8(ps, host.get() + (size_t)b * R * row, rows) != 0) good = false;
-        }
-        copier.join();
-        if (failed) hip_rc = RT_E_HIP;
+        bool good = !hip_rc && rth_ppm_open(path, W, H, 0, &ps) == 0;
+        for (int y = 0; good && y < H; y += R)
+            if (rth_ppm_write_rows_u8(ps, host.get() + (size_t)y * row, std::min(R, H - y)) != 0) good = false;
         if (ps && rth_ppm_close(ps) != 0) good = false;
         ret = good ? 0 : -1;
     }
@@ -386,19 +362,21 @@ int main(int argc, char *argv[]) {
         if (!r) r = rt_render_rows(s, &cam, W, H, 0, H, dimg, &st[0]);
         ph_render = ms_since(t);
         t = Clock::now();
-        // the writer's values as bytes, quantised on the device (3 B per
-        // pixel to the host, copy overlapped with the writer); the floats
-        // only when some value is not 0..255 or --float-out wants them
+        // below 512 MB of floats: the writer's values as bytes, quantised on
+        // the device (3 B per pixel to the host); the floats when some value
+        // is not 0..255, or --float-out wants them, or the image is large
+        // enough for the pinned copy-and-write overlap below (C4, C5: it
+        // hides the copy entirely)
+        const bool big = (size_t)W * H * 3 * sizeof(float) >= (size_t(512) << 20);
         int bytes_rc = 1;
-        if (!r && !float_out && !std::getenv("RT_PPM_FLOATS")) {
+        if (!r && !float_out && !big && !std::getenv("RT_PPM_FLOATS")) {
             double d2h = 0.0;
             bytes_rc = write_ppm_bytes(out, dimg, W, H, r, d2h);
             if (bytes_rc != 1) {           // written (or failed): one phase, reported as the write
                 streamed = true;
                 streamed_wr = bytes_rc;
-                ph_write = ms_since(t);
                 ph_d2h = d2h;
-                d2h_overlapped = true;
+                ph_write = ms_since(t) - d2h;
             }
         }
         t = Clock::now();
@@ -406,8 +384,7 @@ int main(int argc, char *argv[]) {
         // and more: below that the two pinned buffers' allocation costs more
         // than the overlap saves (C3's 201 MB: 37 -> 96 ms; C5's 3.2 GB: 542 ->
         // 361 ms)
-        const bool stream = (size_t)W * H * 3 * sizeof(float) >= (size_t(512) << 20) ||
-                            std::getenv("RT_PPM_BLOCK_ROWS") != nullptr;
+        const bool stream = big || std::getenv("RT_PPM_BLOCK_ROWS") != nullptr;
         if (streamed || r) {
         } else if (!float_out && stream) {
             // one phase, reported as the write

@@ -247,8 +247,10 @@ hipError_t quantize_u8_launch(const float *rgb, size_t n, unsigned char *out, un
 // tests; option counters; rt_kernels.hip RT_COUNT)
 hipError_t render_launch(int maxf, int mode, bool count, const Params &p, unsigned grid, size_t lds_bytes,
                          hipStream_t st);
-hipError_t deinterleave_launch(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
-                               hipStream_t st);
+// gathered row sets -> image order; a row is row_bytes bytes of elements of
+// elem_bytes (4: floats, 1: the writer's bytes)
+hipError_t deinterleave_launch(const void *gathered, size_t row_bytes, size_t elem_bytes, int world, int rows_per,
+                               int H, int block, void *image, hipStream_t st);
 
 }  // namespace rt
 

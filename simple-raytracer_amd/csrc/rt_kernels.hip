@@ -1970,17 +1970,18 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 #endif
 }
 
-// Gathered row sets -> image order (rt_deinterleave_rows): one thread per
-// float4 of an image row; image row y belongs to rank (y / block) % world as
-// its local row (y / (block * world)) * block + y % block.
-__global__ void deinterleave_kernel(const float *__restrict__ gathered, int world, int rows_per, int W, int H,
-                                    int block, float *__restrict__ image) {
+// Gathered row sets -> image order (rt_deinterleave_rows, _u8): image row y
+// belongs to rank (y / block) % world as its local row (y / (block * world)) *
+// block + y % block; a row is n elements of T (16-B vectors when the row's
+// bytes allow, else the row's own element type).
+template <typename T>
+__global__ void deinterleave_kernel(const T *__restrict__ gathered, int world, int rows_per, size_t n, int block,
+                                    T *__restrict__ image) {
     const int y = blockIdx.y;
     const int rank = (y / block) % world;
     const int k = (y / (block * world)) * block + y % block;
-    const size_t n = (size_t)W * 3;
-    const float *src = gathered + ((size_t)rank * rows_per + k) * n;
-    float *dst = image + (size_t)y * n;
+    const T *src = gathered + ((size_t)rank * rows_per + k) * n;
+    T *dst = image + (size_t)y * n;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
 }
@@ -2086,11 +2087,24 @@ hipError_t render_launch(int maxf, int mode, bool count, const Params &p, unsign
                  : launch_maxf<false>(maxf, mode, p, grid, lds_bytes, st);
 }
 
-hipError_t deinterleave_launch(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
-                               hipStream_t st) {
-    const unsigned gx = (unsigned)std::min<size_t>(64, ((size_t)W * 3 + 255) / 256);
-    hipLaunchKernelGGL(deinterleave_kernel, dim3(gx, (unsigned)H), dim3(256), 0, st, gathered, world, rows_per, W, H,
-                       block, image);
+hipError_t deinterleave_launch(const void *gathered, size_t row_bytes, size_t elem_bytes, int world, int rows_per,
+                               int H, int block, void *image, hipStream_t st) {
+    const bool vec = row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(gathered) % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(image) % 16 == 0;
+    const size_t eb = vec ? 16 : elem_bytes, n = row_bytes / eb;
+    const unsigned gx = (unsigned)std::min<size_t>(64, (n + 255) / 256);
+    const dim3 grid(gx, (unsigned)H);
+    if (vec)
+        hipLaunchKernelGGL(deinterleave_kernel<uint4>, grid, dim3(256), 0, st, static_cast<const uint4 *>(gathered),
+                           world, rows_per, n, block, static_cast<uint4 *>(image));
+    else if (eb == 4)
+        hipLaunchKernelGGL(deinterleave_kernel<unsigned>, grid, dim3(256), 0, st,
+                           static_cast<const unsigned *>(gathered), world, rows_per, n, block,
+                           static_cast<unsigned *>(image));
+    else
+        hipLaunchKernelGGL(deinterleave_kernel<unsigned char>, grid, dim3(256), 0, st,
+                           static_cast<const unsigned char *>(gathered), world, rows_per, n, block,
+                           static_cast<unsigned char *>(image));
     return hipGetLastError();
 }
 

@@ -143,17 +143,23 @@ struct StepTimer {
     }
 };
 
-template <typename T, typename P>
-int upload(rt_scene *s, const std::vector<T> &v, P &dst) {
-    size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
-    void *d = nullptr;
-    if (hipMalloc(&d, bytes) != hipSuccess) return RT_E_NOMEM;
-    s->allocs.push_back(d);
-    if (!v.empty() && hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-        return RT_E_HIP;
-    dst = static_cast<P>(d);
-    return RT_OK;
-}
+// Host staging of several device arrays packed into one allocation, each at
+// a 256-B aligned offset (at least one element's room, as the arrays were
+// allocated one by one before round 5)
+struct Arena {
+    std::vector<char> host;
+    size_t reserve(size_t bytes) {
+        const size_t off = (host.size() + 255) / 256 * 256;
+        host.resize(off + std::max<size_t>(16, bytes), 0);
+        return off;
+    }
+    template <typename T>
+    size_t add(const std::vector<T> &v) {
+        const size_t off = reserve(std::max<size_t>(1, v.size()) * sizeof(T));
+        if (!v.empty()) std::memcpy(host.data() + off, v.data(), v.size() * sizeof(T));
+        return off;
+    }
+};
 
 
 // Dynamic LDS of render_kernel: the per-lane shading state, the mode's region
@@ -529,20 +535,40 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
 
     int rc = RT_OK;
     Params &p = s->base;
-    if (!rc) rc = upload(s, in.fscan, p.fscan);
-    if (!rc) rc = upload(s, in.sscan, p.sscan);
-    if (!rc) rc = upload(s, in.ofac, p.ofac);
-    if (!rc) rc = upload(s, in.objs, p.objs);
-    if (!rc) rc = upload(s, in.fsh, p.fsh);
-    if (!rc) rc = upload(s, in.lights, p.lights);
-    std::vector<unsigned char> texels;
+    size_t tex_bytes = 0;
     for (int i = 0; i < desc->n_textures; i++) {
         const rt_texture_desc &T = desc->textures[i];
-        texs[i].w = T.width, texs[i].h = T.height, texs[i].off = (long long)texels.size();
-        texels.insert(texels.end(), T.rgb, T.rgb + (size_t)T.width * T.height * 3);
+        texs[i].w = T.width, texs[i].h = T.height, texs[i].off = (long long)tex_bytes;
+        tex_bytes += (size_t)T.width * T.height * 3;
     }
-    if (!rc) rc = upload(s, texels, p.texels);
-    if (!rc) rc = upload(s, texs, p.texs);
+    // every per-object array in one device allocation, filled by one copy
+    // from one host staging buffer (eight allocations and eight pageable
+    // copies cost ~8 ms of a one-shot run)
+    {
+        Arena a;
+        const size_t o_fscan = a.add(in.fscan), o_sscan = a.add(in.sscan), o_ofac = a.add(in.ofac);
+        const size_t o_objs = a.add(in.objs), o_fsh = a.add(in.fsh), o_lights = a.add(in.lights);
+        const size_t o_texels = a.reserve(tex_bytes), o_texs = a.add(texs);
+        for (int i = 0; i < desc->n_textures; i++) {
+            const rt_texture_desc &T = desc->textures[i];
+            std::memcpy(a.host.data() + o_texels + (size_t)texs[i].off, T.rgb, (size_t)T.width * T.height * 3);
+        }
+        char *d = nullptr;
+        if (hipMalloc((void **)&d, a.host.size()) != hipSuccess) {
+            rc = RT_E_NOMEM;
+        } else {
+            s->allocs.push_back(d);
+            if (hipMemcpy(d, a.host.data(), a.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = RT_E_HIP;
+            p.fscan = reinterpret_cast<const float4 *>(d + o_fscan);
+            p.sscan = reinterpret_cast<const float4 *>(d + o_sscan);
+            p.ofac = reinterpret_cast<const float *>(d + o_ofac);
+            p.objs = reinterpret_cast<const ObjK *>(d + o_objs);
+            p.fsh = reinterpret_cast<const FaceShadeK *>(d + o_fsh);
+            p.lights = reinterpret_cast<const LightK *>(d + o_lights);
+            p.texels = reinterpret_cast<const unsigned char *>(d + o_texels);
+            p.texs = reinterpret_cast<const TexK *>(d + o_texs);
+        }
+    }
     tm.mark("uploads");
     if (!rc && !(s->stream = take_stream(device)) &&
         hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
@@ -628,13 +654,17 @@ int rt_device_init(int device) {
     // the runtime's lazily made state: device memory, the staging paths of
     // both copy directions, a hardware queue (a stream kept for the next
     // rt_scene_create), the kernels' code object (an occupancy query)
+    // (copies of 4 KB and of 1 MB: the first copy of each size class pays
+    // its own staging setup -- a 33-KB counter read cost 7.5 ms after a
+    // 4-KB warm-up)
     void *d = nullptr;
-    unsigned char h[4096] = {0};
+    std::vector<unsigned char> h((size_t)1 << 20, 0);
     int rc = RT_OK;
-    if (hipMalloc(&d, sizeof h) != hipSuccess) return RT_E_NOMEM;
-    if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
-        rc = RT_E_HIP;
+    if (hipMalloc(&d, h.size()) != hipSuccess) return RT_E_NOMEM;
+    for (size_t n : {(size_t)4096, h.size()})
+        if (hipMemcpy(d, h.data(), n, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(h.data(), d, n, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = RT_E_HIP;
     (void)hipFree(d);
     tm.mark("memory + copies");
     hipStream_t st = nullptr;
@@ -770,8 +800,8 @@ int rt_render_pixels(rt_scene *s, const rt_camera *cam, int W, int H, const int 
     return RT_OK;
 }
 
-int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
-                         void *hip_stream) {
+static int deinterleave(const void *gathered, size_t elem_bytes, int world, int rows_per, int W, int H, int block,
+                        void *image, void *hip_stream) {
     if (!gathered || !image || world < 1 || rows_per < 1 || W < 1 || H < 1 || block < 1) return RT_E_INVALID;
     if (H > 65535) return RT_E_UNSUPPORTED;
     // every image row's source row must exist: each rank's row count <= rows_per
@@ -781,9 +811,20 @@ int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, 
         for (int b = r; b < nblocks; b += world) rows += std::min(block, H - b * block);
         if (rows > rows_per) return RT_E_INVALID;
     }
-    return deinterleave_launch(gathered, world, rows_per, W, H, block, image, (hipStream_t)hip_stream) == hipSuccess
+    return deinterleave_launch(gathered, (size_t)W * 3 * elem_bytes, elem_bytes, world, rows_per, H, block, image,
+                               (hipStream_t)hip_stream) == hipSuccess
                ? RT_OK
                : RT_E_HIP;
+}
+
+int rt_deinterleave_rows(const float *gathered, int world, int rows_per, int W, int H, int block, float *image,
+                         void *hip_stream) {
+    return deinterleave(gathered, sizeof(float), world, rows_per, W, H, block, image, hip_stream);
+}
+
+int rt_deinterleave_rows_u8(const unsigned char *gathered, int world, int rows_per, int W, int H, int block,
+                            unsigned char *image, void *hip_stream) {
+    return deinterleave(gathered, 1, world, rows_per, W, H, block, image, hip_stream);
 }
 
 int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *flag, void *hip_stream) {

@@ -92,7 +92,7 @@ HIP_SYMBOLS = ["rt_device_count", "rt_device_init", "rt_scene_create", "rt_scene
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_scene_debug_ub_pixels",
-               "rt_deinterleave_rows", "rt_quantize_u8",
+               "rt_deinterleave_rows", "rt_deinterleave_rows_u8", "rt_quantize_u8",
                "rt_strerror"]
 
 
@@ -171,6 +171,9 @@ def hip_lib() -> C.CDLL:
         if hasattr(L, "rt_deinterleave_rows"):
             L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                C.c_void_p, C.c_void_p]
+        if hasattr(L, "rt_deinterleave_rows_u8"):  # absent from round-1..4 libraries (A/B baselines)
+            L.rt_deinterleave_rows_u8.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                  C.c_void_p, C.c_void_p]
         if hasattr(L, "rt_quantize_u8"):           # absent from round-1..3 libraries (A/B baselines)
             L.rt_quantize_u8.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
@@ -269,6 +272,16 @@ def quantize_u8_device(rgb_ptr: int, n: int, out_ptr: int, flag_ptr: int, stream
     as bytes; bit 0 of the uint32 at flag_ptr is set when a value is not 0..255."""
     _check(hip_lib().rt_quantize_u8(C.c_void_p(rgb_ptr), n, C.c_void_p(out_ptr), C.c_void_p(flag_ptr),
                                     C.c_void_p(stream)), "rt_quantize_u8")
+
+
+def deinterleave_rows_device(gathered_ptr: int, world: int, rows_per: int, W: int, H: int, block: int,
+                             image_ptr: int, u8: bool, stream: int = 0) -> None:
+    """rt_deinterleave_rows(_u8) on device buffers: `world` gathered row sets
+    (rows_per x W x 3 floats or bytes each) -> the H x W x 3 image in row order."""
+    L = hip_lib()
+    f = L.rt_deinterleave_rows_u8 if u8 else L.rt_deinterleave_rows
+    _check(f(C.c_void_p(gathered_ptr), world, rows_per, W, H, block, C.c_void_p(image_ptr), C.c_void_p(stream)),
+           "rt_deinterleave_rows")
 
 
 def write_ppm(path: str, rgb: np.ndarray, threads: int = 0) -> None:

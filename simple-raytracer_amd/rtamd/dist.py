@@ -53,12 +53,18 @@ class ImageGather:
             raise ValueError(f"gather format {fmt!r}")
         self.targets = self.image = None
         self.index = []
+        self.W, self.rows_per = W, rows_per
         if world > 1 and rank == 0:
-            self.targets = [torch.empty_like(self.send) for _ in range(world)]
+            # the N gathered row sets in one buffer (rank r's at [r]): one
+            # device kernel puts them in image order (rt_deinterleave_rows
+            # / _u8; N index_copy_ on CPU tensors)
+            self.gathered = torch.empty((world,) + tuple(self.send.shape), dtype=self.send.dtype, device=device)
+            self.targets = list(self.gathered.unbind(0))
             self.image = torch.empty((H, W, 3), dtype=self.send.dtype, device=device)
-            for r in range(world):
-                rows = image_rows(H, world, r)
-                self.index.append(torch.tensor(rows, dtype=torch.long, device=device) if rows else None)
+            if not self.send.is_cuda:
+                for r in range(world):
+                    rows = image_rows(H, world, r)
+                    self.index.append(torch.tensor(rows, dtype=torch.long, device=device) if rows else None)
 
     def gather(self, dist):
         """Collect every rank's rows on rank 0 (one fixed-count collective) and
@@ -81,6 +87,12 @@ class ImageGather:
             dist.gather(self.send, self.targets, dst=0)
         if self.rank != 0:
             return None
+        if self.image.is_cuda:
+            import rtamd
+            rtamd.deinterleave_rows_device(self.gathered.data_ptr(), self.world, self.rows_per, self.W, self.H,
+                                           BLOCK, self.image.data_ptr(), self.fmt == "u8",
+                                           self.torch.cuda.current_stream().cuda_stream)
+            return self.image
         for r, idx in enumerate(self.index):
             if idx is not None:
                 self.image.index_copy_(0, idx, self.targets[r][: idx.numel()])

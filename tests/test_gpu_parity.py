@@ -1077,20 +1077,28 @@ def test_special_cases_on_the_bvh(cfg, accel, tmp_path):
                                           tests=dict(box=st.box_tests, face=st.face_tests, sphere=st.sphere_tests))
 
 
-def test_deinterleave_rows_device():
-    """rt_deinterleave_rows puts gathered row sets (rth_row_set's dealing)
-    back in image order on the device, for ragged heights and several ranks."""
+@pytest.mark.parametrize("u8", [False, True])
+def test_deinterleave_rows_device(u8):
+    """rt_deinterleave_rows (floats) and rt_deinterleave_rows_u8 (the
+    writer's bytes) put gathered row sets (rth_row_set's dealing) back in
+    image order on the device, for ragged heights, several ranks, and row
+    widths with and without the 16-B vector path (W * 3 * element bytes a
+    multiple of 16 or not)."""
     torch = pytest.importorskip("torch")
     import ctypes as C
     from rtamd.dist import image_rows, row_set
     L = rtamd.hip_lib()
-    for H, world in ((67, 3), (8, 2), (130, 8), (5, 1)):
-        W = 13
+    f = L.rt_deinterleave_rows_u8 if u8 else L.rt_deinterleave_rows
+    for H, world, W in ((67, 3, 13), (8, 2, 16), (130, 8, 13), (5, 1, 64), (41, 4, 48)):
         per = row_set(H, world, 0)[4]
-        g = torch.rand((world, per, W, 3), dtype=torch.float32, device="cuda:0")
-        img = torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
-        rc = L.rt_deinterleave_rows(C.c_void_p(g.data_ptr()), world, per, W, H, 8, C.c_void_p(img.data_ptr()),
-                                    C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if u8:
+            g = torch.randint(0, 256, (world, per, W, 3), dtype=torch.uint8, device="cuda:0")
+            img = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        else:
+            g = torch.rand((world, per, W, 3), dtype=torch.float32, device="cuda:0")
+            img = torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0")
+        rc = f(C.c_void_p(g.data_ptr()), world, per, W, H, 8, C.c_void_p(img.data_ptr()),
+               C.c_void_p(torch.cuda.current_stream().cuda_stream))
         assert rc == 0
         torch.cuda.synchronize()
         want = torch.empty_like(img)
@@ -1098,9 +1106,9 @@ def test_deinterleave_rows_device():
             rows = image_rows(H, world, r)
             if rows:
                 want[rows] = g[r, : len(rows)]
-        assert torch.equal(img, want), (H, world)
-        assert L.rt_deinterleave_rows(C.c_void_p(g.data_ptr()), world, per - 1 if per > 1 else 0, W, H, 8,
-                                      C.c_void_p(img.data_ptr()), None) == -1
+        assert torch.equal(img, want), (H, world, W)
+        assert f(C.c_void_p(g.data_ptr()), world, per - 1 if per > 1 else 0, W, H, 8,
+                 C.c_void_p(img.data_ptr()), None) == -1
 
 
 @pytest.mark.parametrize("block", ["100000", "1", "7", "64"])

@@ -27,6 +27,10 @@ def main():
     from rtamd import scenes as gen
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     keep = "--keep" in sys.argv
+    # --floats: the P3 file from the float image (RT_PPM_FLOATS), for an A/B
+    # against the default byte path (device-quantised, 3 B per pixel)
+    floats = "--floats" in sys.argv
+    tag = "_floats" if floats else ""
     cli = os.path.join(ROOT, "simple-raytracer_amd", "lib", "rt")
     od = os.path.join(ROOT, "gpurun_out")
     os.makedirs(od, exist_ok=True)
@@ -39,7 +43,7 @@ def main():
         # RT_TIMING: the library's own step times (scene creation, BVH upload,
         # first launch) on stderr, kept in the record
         r = subprocess.run(cmd, cwd=d, capture_output=True, text=True, timeout=600,
-                           env={**os.environ, "RT_TIMING": "1"})
+                           env={**os.environ, "RT_TIMING": "1", **({"RT_PPM_FLOATS": "1"} if floats else {})})
         wall = time.perf_counter() - t0
         if r.returncode != 0:
             print(f"{cfg}: rt failed rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}", flush=True)
@@ -53,7 +57,7 @@ def main():
         ppm = os.path.splitext(path)[0] + ".ppm"
         if not keep and os.path.exists(ppm):
             os.remove(ppm)
-        with open(os.path.join(od, f"e2e_{cfg}.json"), "w") as f:
+        with open(os.path.join(od, f"e2e_{cfg}{tag}.json"), "w") as f:
             json.dump(j, f, indent=1)
         print(json.dumps(j), flush=True)
 

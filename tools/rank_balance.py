@@ -108,7 +108,7 @@ def main():
 
     # Rank 0's per-frame work beyond its render at N > 1 (bench.py step():
     # every rank quantises its strip, rt_quantize_u8; rank 0 then launches the
-    # gather and puts N gathered strips in image order with N index_copy_),
+    # gather and puts the N gathered row sets in image order, one device kernel),
     # measured on this GPU with the buffers of an N-rank run; the collective's
     # launch by a one-rank NCCL gather of the strip (its data path, xGMI, is
     # the estimate below)
@@ -116,7 +116,6 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    from rtamd.dist import image_rows
 
     def timed(fn, reps=30):
         fn()
@@ -133,20 +132,18 @@ def main():
         strip = torch.zeros((per, W, 3), dtype=torch.float32, device="cuda")
         send = torch.zeros((per, W, 3), dtype=torch.uint8 if fmt == "u8" else torch.float32, device="cuda")
         flag = torch.zeros(1, dtype=torch.int32, device="cuda")
-        targets = [torch.zeros_like(send) for _ in range(n)]
+        gathered = torch.zeros((n, per, W, 3), dtype=send.dtype, device="cuda")
         image = torch.empty((H, W, 3), dtype=send.dtype, device="cuda")
-        idx = [torch.tensor(image_rows(H, n, r), dtype=torch.long, device="cuda") for r in range(n)]
         q_ms = timed(lambda: quantize_u8_device(rtamd, torch, strip, send, flag)) if fmt == "u8" else 0.0
 
-        def scatter():
-            for r in range(n):
-                if idx[r].numel():
-                    image.index_copy_(0, idx[r], targets[r][: idx[r].numel()])
+        def scatter():                       # rank 0: the gathered row sets -> image order, one kernel
+            rtamd.deinterleave_rows_device(gathered.data_ptr(), n, per, W, H, 8, image.data_ptr(), fmt == "u8",
+                                           torch.cuda.current_stream().cuda_stream)
         copy_ms = timed(scatter)
         one = [torch.zeros_like(send)]
         launch_ms = timed(lambda: dist.gather(send, one, dst=0))
-        del strip, send, targets, image
-        return dict(quantise_ms=round(q_ms, 4), index_copy_ms=round(copy_ms, 4),
+        del strip, send, gathered, image
+        return dict(quantise_ms=round(q_ms, 4), deinterleave_ms=round(copy_ms, 4),
                     gather_launch_ms=round(launch_ms, 4), total_ms=round(q_ms + copy_ms + launch_ms, 4))
 
     base = None
@@ -168,7 +165,7 @@ def main():
         p = [x["pipelined_ms"] for x in ranks]
         strip_bytes = row_set(H, n, 0)[4] * W * 3 * bpp
         gather_ms = strip_bytes / (XGMI_GBPS * 1e9) * 1e3 if n > 1 else 0.0
-        # rank 0's extra work (quantise, index_copy_ x N, the gather's launch)
+        # rank 0's extra work (quantise, de-interleave, the gather's launch)
         # counted whole, like the gather: it overlaps the next frames' renders
         # only partly
         extra = rank0_extra(n) if n > 1 else dict(total_ms=0.0)
