@@ -4,9 +4,10 @@ subprocess per (library variant, runtime options) pair.
 
   python tools/ab.py --rounds 2 --config C3 base: w4:lib_w4 leaf4::bvh_leaf=4 ...
 
-Each spec is  name:libdir:opt=v,opt=v  (libdir relative to
-simple-raytracer_amd/, empty = lib).  Results -> gpurun_out/ab.jsonl + a
-summary table on stdout."""
+Each spec is  name:libdir:opt=v,opt=v[:--arg=v,--arg=v]  (libdir relative
+to simple-raytracer_amd/, empty = lib; the last field: extra bench.py
+arguments, e.g. --inflight=3).  Results -> gpurun_out/ab.jsonl + a summary
+table on stdout."""
 from __future__ import annotations
 
 import argparse
@@ -32,7 +33,7 @@ def main():
     res: dict[str, list] = {}
     for r in range(a.rounds):
         for spec in a.specs:
-            name, lib, opts = (spec.split(":") + ["", ""])[:3]
+            name, lib, opts, bargs = (spec.split(":") + ["", "", ""])[:4]
             env = dict(os.environ)
             if lib:
                 env["RTAMD_LIB_DIR"] = os.path.join(ROOT, "simple-raytracer_amd", lib)
@@ -40,6 +41,7 @@ def main():
                    str(a.steps), "--config", a.config]
             for o in filter(None, opts.split(",")):
                 cmd += ["--option", o]
+            cmd += [x for x in bargs.split(",") if x]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
             line = next((l for l in p.stdout.splitlines() if l.startswith("{")), None)
             if p.returncode != 0 or line is None:
