@@ -182,6 +182,10 @@ static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack -
 #endif
 constexpr int kBlock = RT_BLOCK;
 constexpr long long kCounters = 1;       // option counters default (the instantiation without is ~4 % faster)
+#ifndef RT_FRAME_SHARE
+#define RT_FRAME_SHARE 1                 // option frame_share's automatic value with frames in flight
+#endif
+constexpr long long kFrameShare = RT_FRAME_SHARE;
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

@@ -409,12 +409,13 @@ def test_prepare_then_render():
         gs.prepare(cam, 0, H)                 # (1 x H is a valid image: the seam's NaN camera)
 
 
-@pytest.mark.parametrize("inflight", [2, 3])
-def test_frames_in_flight(inflight):
+@pytest.mark.parametrize("inflight,share", [(2, -1), (3, -1), (2, 1), (3, 4)])
+def test_frames_in_flight(inflight, share):
     """Option "inflight": renders issued on different caller streams run on the
-    scene's render slots and overlap.  Every frame equals the one-at-a-time
-    render bit for bit, its counters are its own, and work queued on a caller
-    stream after a render sees the finished image."""
+    scene's render slots and overlap (each on the grid share "frame_share"
+    gives it: auto = half the occupancy grid).  Every frame equals the
+    one-at-a-time render bit for bit, its counters are its own, and work queued
+    on a caller stream after a render sees the finished image."""
     torch = pytest.importorskip("torch")
     hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
     hs.set_depth(4)
@@ -423,6 +424,7 @@ def test_frames_in_flight(inflight):
     gs = rtamd.GpuScene(hs)
     ref, st = gs.render_rows(cam, W, H, 0, H)
     gs.set_option("inflight", inflight)
+    gs.set_option("frame_share", share)
     streams = [torch.cuda.Stream() for _ in range(inflight)]
     frames = 2 * inflight + 1
     outs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(frames)]
@@ -445,6 +447,9 @@ def test_frames_in_flight(inflight):
     assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9))
     with pytest.raises(rtamd.RTError):
         gs.set_option("inflight", 9)
+    for bad in (0, 9, -2):
+        with pytest.raises(rtamd.RTError):
+            gs.set_option("frame_share", bad)
 
 
 def test_abi_errors():

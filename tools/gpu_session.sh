@@ -4,7 +4,7 @@
 # fault or a timeout).  Usage:
 #   gpurun -- 'bash tools/gpu_session.sh NAME STEP [STEP ...]'
 # STEP: tests | bench[:CONFIG] | ab:CONFIG:ROUNDS:STEPS:SPEC,SPEC,... |
-#       prof:CONFIG | pmc:CONFIG | e2e | phases:CONFIG[:OPTS] | balance:CONFIG[:NS] | cmd:NAME:CMD
+#       prof:CONFIG | pmc:CONFIG[:LIBDIR] | e2e | phases:CONFIG[:OPTS] | balance:CONFIG[:NS] | cmd:NAME:CMD
 set -o pipefail
 name=$1; shift
 out=gpurun_out/$name
@@ -29,19 +29,22 @@ for step in "$@"; do
         --cpu-baseline off) > "$out/prof_$a.log" 2>&1 || { tail -20 "$out/prof_$a.log"; exit 1; } ;;
     pmc)
       # FETCH / WRITE bytes and the SQ/TA/TCC counters of one frame, one
-      # rocprofv3 pass per counter group (never combined with tracing)
-      i=0
+      # rocprofv3 pass per counter group (never combined with tracing);
+      # b: a library variant's directory under simple-raytracer_amd/ (lib_n8)
+      i=0; tag=$a${b:+_$b}
+      if [ -n "$b" ]; then export RTAMD_LIB_DIR=$GRAFT_REPO_ROOT/simple-raytracer_amd/$b; else unset RTAMD_LIB_DIR; fi
       for pass in "FETCH_SIZE" "WRITE_SIZE" \
           "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" \
           "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_THREAD_CYCLES_VALU TA_BUSY_avr" \
           "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum"; do
         i=$((i+1))
-        (cd /tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $pass -d "$GRAFT_REPO_ROOT/$out/pmc_$a/p$i" \
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $pass -d "$GRAFT_REPO_ROOT/$out/pmc_$tag/p$i" \
           -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config "$a" --cpu-baseline off \
-          --steps 1 --warmup 0 --inflight 1 --count-render off) > "$out/pmc_${a}_p$i.log" 2>&1 \
-          || { tail -20 "$out/pmc_${a}_p$i.log"; exit 1; }
+          --steps 1 --warmup 0 --inflight 1 --count-render off) > "$out/pmc_${tag}_p$i.log" 2>&1 \
+          || { tail -20 "$out/pmc_${tag}_p$i.log"; exit 1; }
       done
-      RENDERS=2 python3 tools/pmc_summary.py "$out/pmc_$a" > "$out/${a}_pmc.json" ;;
+      unset RTAMD_LIB_DIR
+      RENDERS=2 python3 tools/pmc_summary.py "$out/pmc_$tag" > "$out/${tag}_pmc.json" ;;
     e2e)
       # a: extra flags (floats: the float writer, RT_PPM_FLOATS)
       timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 ${a:+--$a} > "$out/e2e$a.txt" 2>&1 || { tail -20 "$out/e2e$a.txt"; exit 1; } ;;

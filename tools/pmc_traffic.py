@@ -11,7 +11,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-METHOD = ("rocprofv3 --kernel-trace --pmc, one counter group per pass (tools/final_session.sh, bench.py "
+METHOD = ("rocprofv3 --kernel-trace --pmc, one counter group per pass (tools/gpu_session.sh pmc step, bench.py "
           "--inflight 1 --steps 1 --warmup 0 --count-render off: 2 renders of the kernel without counters per pass, RENDERS=2); read = 2 x FETCH_SIZE x 1024 "
           "(gfx950 correction, MI355X_MICROARCH.md HBM), write = WRITE_SIZE x 1024")
 
