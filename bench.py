@@ -114,7 +114,10 @@ def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
     # fall back to this repo's C restatement on all cores (a port, not the reference)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_py import OracleScene
-    o = OracleScene(path)
+    o = OracleScene(path, cwd=d)             # (a textured scene names its texture relative to d)
+    if o.rc:
+        raise RuntimeError(f"oracle could not load {path}: {o.msg}")
+    o.set_depth(gen.CONFIGS[config]["depth"])
     t0 = time.perf_counter()
     _, cnt = o.render(threads=0)
     dt = time.perf_counter() - t0
@@ -141,7 +144,9 @@ def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0, threads:
     def run(side: int):
         d = tempfile.mkdtemp(prefix="rtamd_port_")
         path = gen.write_scene(d, config, w=side, h=side, tag=f"{config}_{side}_port")
-        o = OracleScene(path)
+        o = OracleScene(path, cwd=d)         # (a textured scene names its texture relative to d)
+        if o.rc:
+            raise RuntimeError(f"oracle could not load {path}: {o.msg}")
         o.set_depth(gen.CONFIGS[config]["depth"])
         t0 = time.perf_counter()
         _, cnt = o.render(threads=threads)

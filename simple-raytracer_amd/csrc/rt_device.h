@@ -183,9 +183,13 @@ static_assert(kStackMax % kSpill == 0 && kStackMax / kSpill < 200 && kLdsStack -
 constexpr int kBlock = RT_BLOCK;
 constexpr long long kCounters = 1;       // option counters default (the instantiation without is ~4 % faster)
 #ifndef RT_FRAME_SHARE
-#define RT_FRAME_SHARE 1                 // option frame_share's automatic value with frames in flight
+#define RT_FRAME_SHARE 2                 // option frame_share's automatic value for small frames in flight
 #endif
 constexpr long long kFrameShare = RT_FRAME_SHARE;
+#ifndef RT_FRAME_SHARE_ITEMS
+#define RT_FRAME_SHARE_ITEMS 32          // ... for frames of at most this many work items per lane of the grid
+#endif
+constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

@@ -79,7 +79,7 @@ struct rt_scene {
     long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
     long long opt_counters = kCounters;  // 1: the counting kernel (rt_stats' rays, events, tests); 0: none
     long long opt_frame_share = -1;    // the occupancy-sized grid / this: frames in flight that run side by
-                                       // side (-1 auto: kFrameShare when inflight > 1, else 1)
+                                       // side (-1 auto: kFrameShare for small frames with inflight > 1, else 1)
     long long opt_recursive = 0;       // test hook: 1 forces the recursive instantiation (MAXF by depth) on a
                                        // scene without reflecting / refracting materials (no last-light skip)
     int last_light_skip_auto = 0;      // Params::last_light_skip when exact for the scene
@@ -218,15 +218,20 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     tm.mark("occupancy");
     if (nb < 1) nb = 1;
     long long grid = s->opt_grid > 0 ? s->opt_grid : (long long)nb * s->num_cu - s->opt_reserve;
-    // Frames in flight (option inflight > 1) run side by side on a share of
-    // the CUs each: a frame's tail -- its waves finishing the pixels they hold
-    // once the work is gone, a workgroup's slots freed only when its four
-    // waves are done -- then idles only its own share while the other frames
-    // go on (C3's N = 8 share 1.83 -> 1.67 ms per frame at half
-    // the grid)
+    // Short frames in flight (option inflight > 1, at most kFrameShareItems
+    // work items per lane of the occupancy-sized grid: C3's rows of one rank
+    // at N = 2 / 4 / 8, 25.6 / 12.8 / 6.4 per lane) run side by side on a
+    // share of the CUs each: a frame's tail -- its waves finishing the pixels
+    // they hold once the work is gone, a workgroup's slots freed only when its
+    // four waves are done -- then idles only its own share while the other
+    // frames go on.  C3 pipelined at half the grid: N = 8 1.763 -> 1.649 ms
+    // per frame (a third: 1.663, a quarter: 1.752), N = 4 3.19 -> 3.05,
+    // N = 2 6.09 -> 5.89; a whole C3 frame (51 per lane) gains nothing from
+    // it (-1.1 % over 60 steps; profiles/r05/frame_share/)
     if (s->opt_grid <= 0) {
+        const bool small = (unsigned long long)p.total <= (unsigned long long)grid * kBlock * kFrameShareItems;
         const long long share = s->opt_frame_share > 0 ? s->opt_frame_share
-                                : s->slots.size() > 1 ? kFrameShare : 1;
+                                : s->slots.size() > 1 && small ? kFrameShare : 1;
         grid = std::max(1LL, grid / share);
     }
     long long need = ((long long)p.total + kBlock - 1) / kBlock;

@@ -68,47 +68,52 @@ class OracleScene:
 
     @property
     def width(self) -> int:
-        return lib().oracle_width(self._h)
+        return lib().oracle_width(self._loaded())
 
     @property
     def height(self) -> int:
-        return lib().oracle_height(self._h)
+        return lib().oracle_height(self._loaded())
 
     def set_depth(self, d: int) -> None:
-        lib().oracle_set_depth(self._h, d)
+        lib().oracle_set_depth(self._loaded(), d)
+
+    def _loaded(self):
+        if not self._h:
+            raise RuntimeError(f"scene not loaded (rc {self.rc}): {self.msg}")
+        return self._h
 
     def counts(self):
         nf, ns, nl = C.c_int(), C.c_int(), C.c_int()
-        lib().oracle_counts_objects(self._h, C.byref(nf), C.byref(ns), C.byref(nl))
+        lib().oracle_counts_objects(self._loaded(), C.byref(nf), C.byref(ns), C.byref(nl))
         return nf.value, ns.value, nl.value
 
     def objects(self) -> np.ndarray:
         nf, ns, _ = self.counts()
         out = np.zeros((nf + ns, 48), dtype=np.float32)
         for i in range(nf + ns):
-            lib().oracle_object(self._h, i, out[i].ctypes.data)
+            lib().oracle_object(self._loaded(), i, out[i].ctypes.data)
         return out
 
     def lights(self) -> np.ndarray:
         _, _, nl = self.counts()
         out = np.zeros((nl, 8), dtype=np.float32)
         for i in range(nl):
-            lib().oracle_light(self._h, i, out[i].ctypes.data)
+            lib().oracle_light(self._loaded(), i, out[i].ctypes.data)
         return out
 
     def globals(self) -> np.ndarray:
         out = np.zeros(6, dtype=np.float32)
-        lib().oracle_globals(self._h, out.ctypes.data)
+        lib().oracle_globals(self._loaded(), out.ctypes.data)
         return out
 
     def texture(self, i: int) -> np.ndarray:
         w, h, p = C.c_int(), C.c_int(), C.POINTER(C.c_ubyte)()
-        lib().oracle_texture(self._h, i, C.byref(w), C.byref(h), C.byref(p))
+        lib().oracle_texture(self._loaded(), i, C.byref(w), C.byref(h), C.byref(p))
         return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
 
     def camera(self, W: int, H: int) -> np.ndarray:
         out = np.zeros(12, dtype=np.float32)
-        lib().oracle_camera(self._h, W, H, out.ctypes.data)
+        lib().oracle_camera(self._loaded(), W, H, out.ctypes.data)
         return out
 
     def render(self, W: int | None = None, H: int | None = None, rows=None, threads: int = 0):
@@ -118,7 +123,7 @@ class OracleScene:
         rows = np.arange(H, dtype=np.int32) if rows is None else np.asarray(rows, dtype=np.int32)
         out = np.empty((len(rows), W, 3), dtype=np.float32)
         cnt = np.zeros(6, dtype=np.int64)
-        lib().oracle_render_rows(self._h, W, H, rows.ctypes.data, len(rows), threads, out.ctypes.data,
+        lib().oracle_render_rows(self._loaded(), W, H, rows.ctypes.data, len(rows), threads, out.ctypes.data,
                                  cnt.ctypes.data)
         names = ["primary", "shadow", "refraction", "reflection", "skip_trans", "ub_back"]
         return out, dict(zip(names, (int(c) for c in cnt)))
@@ -128,7 +133,7 @@ class OracleScene:
         xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
         out = np.empty((len(xy), 3), dtype=np.float32)
         cnt = np.zeros(6, dtype=np.int64)
-        lib().oracle_render_pixels(self._h, W, H, xy.ctypes.data, len(xy), threads, out.ctypes.data,
+        lib().oracle_render_pixels(self._loaded(), W, H, xy.ctypes.data, len(xy), threads, out.ctypes.data,
                                    cnt.ctypes.data)
         names = ["primary", "shadow", "refraction", "reflection", "skip_trans", "ub_back"]
         return out, dict(zip(names, (int(c) for c in cnt)))

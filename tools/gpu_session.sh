@@ -43,8 +43,8 @@ for step in "$@"; do
           --steps 1 --warmup 0 --inflight 1 --count-render off) > "$out/pmc_${tag}_p$i.log" 2>&1 \
           || { tail -20 "$out/pmc_${tag}_p$i.log"; exit 1; }
       done
-      unset RTAMD_LIB_DIR
-      RENDERS=2 python3 tools/pmc_summary.py "$out/pmc_$tag" > "$out/${tag}_pmc.json" ;;
+      RENDERS=2 python3 tools/pmc_summary.py "$out/pmc_$tag" > "$out/${tag}_pmc.json"
+      unset RTAMD_LIB_DIR ;;
     e2e)
       # a: extra flags (floats: the float writer, RT_PPM_FLOATS)
       timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 ${a:+--$a} > "$out/e2e$a.txt" 2>&1 || { tail -20 "$out/e2e$a.txt"; exit 1; } ;;
