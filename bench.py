@@ -57,7 +57,8 @@ def parse_args():
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-sample", type=int, default=256,
-                    help="cpu_baseline: the reference renders the same scene at NxN")
+                    help="CPU legs: the reference renders the same scene at up to NxN (the port at up to "
+                         "8N x 8N), sized for ~15 s / ~10 s (sized_run)")
     ap.add_argument("--option", action="append", default=[],
                     help="kernel option key=value (rt_scene_set_option)")
     ap.add_argument("--inflight", type=int, default=0,
@@ -92,38 +93,53 @@ def scene_dir() -> str:
     return d
 
 
-def cpu_baseline(config: str, sample: int, gpu_rays_fn) -> dict | None:
+def sized_run(run, target_s: float, cap: int, side: int = 8):
+    """A CPU leg's bounded sample: square renders of the config's scene from
+    side x side, doubling while one takes under 1/16 of target_s, then one
+    render sized for ~target_s seconds (at most cap x cap).  A 100 000-sphere
+    scene renders a few hundred rays per second on one core, so a fixed
+    sample would take minutes there and milliseconds on C2.  Each render is
+    logged to stderr (a GPU lease kills a run that is silent for minutes).
+    run(side) -> (rays, seconds); returns (rays, seconds, side)."""
+    def timed(n):
+        r, dt = run(n)
+        print(f"[bench] cpu leg: {n}x{n}, {r} rays, {dt:.2f} s", file=sys.stderr, flush=True)
+        return r, dt
+    r, dt = timed(side)
+    while dt < target_s / 16 and side * 2 <= cap:
+        side *= 2
+        r, dt = timed(side)
+    new = int(min(cap, side * (target_s / max(dt, 1e-3)) ** 0.5)) // 8 * 8
+    if new > side:
+        side = new
+        r, dt = timed(side)
+    return r, dt, side
+
+
+def cpu_baseline(config: str, sample: int, gpu_rays_fn, target_s: float = 15.0) -> dict | None:
     """The REAL reference (oracle/_ref/SimpleRayTracer, compiled from the
     reference's own sources by oracle/Makefile) timed on this host's cores on a
-    bounded sample: the same seeded scene at sample x sample pixels (the whole
-    field of view, 1/(W*H/sample^2) of the pixels).  Rays of the sample are
-    counted by the GPU path on the same scene file (counts are parity-tested
-    equal to the reference's TraceRay calls)."""
+    bounded sample: the same seeded scene at side x side pixels (the whole
+    field of view), side <= sample chosen for ~target_s seconds (sized_run).
+    Rays of the sample are counted by the GPU path on the same scene file
+    (counts are parity-tested equal to the reference's TraceRay calls)."""
     from rtamd import scenes as gen
     ref = os.path.join(ROOT, "oracle", "_ref", "SimpleRayTracer")
-    d = tempfile.mkdtemp(prefix="rtamd_cpu_")
-    path = gen.write_scene(d, config, w=sample, h=sample, tag=f"{config}_{sample}")
-    rays = gpu_rays_fn(path)
-    if os.path.exists(ref):
+    if not os.path.exists(ref):
+        return None                          # (cpu_port_baseline times this repo's port beside it)
+
+    def run(side: int):
+        d = tempfile.mkdtemp(prefix="rtamd_cpu_")
+        path = gen.write_scene(d, config, w=side, h=side, tag=f"{config}_{side}")
+        rays = gpu_rays_fn(path)
         t0 = time.perf_counter()
         subprocess.run([ref, os.path.basename(path)], cwd=d, check=True, stdout=subprocess.DEVNULL)
-        dt = time.perf_counter() - t0
-        return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference", "host": host_cores(),
-                "sample": f"{config} scene at {sample}x{sample} (full field of view), {rays} rays, "
-                          f"{dt:.1f} s, single-threaded reference binary"}
-    # fall back to this repo's C restatement on all cores (a port, not the reference)
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_py import OracleScene
-    o = OracleScene(path, cwd=d)             # (a textured scene names its texture relative to d)
-    if o.rc:
-        raise RuntimeError(f"oracle could not load {path}: {o.msg}")
-    o.set_depth(gen.CONFIGS[config]["depth"])
-    t0 = time.perf_counter()
-    _, cnt = o.render(threads=0)
-    dt = time.perf_counter() - t0
-    r = sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection"))
-    return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": os.cpu_count(), "kind": "port",
-            "sample": f"{config} scene at {sample}x{sample}, oracle restatement, {dt:.1f} s"}
+        return rays, time.perf_counter() - t0
+
+    rays, dt, side = sized_run(run, target_s, sample)
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference", "host": host_cores(),
+            "sample": f"{config} scene at {side}x{side} (full field of view), {rays} rays, "
+                      f"{dt:.1f} s, single-threaded reference binary"}
 
 
 def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0, threads: int | None = None) -> dict:
@@ -132,9 +148,9 @@ def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0, threads:
     rows on every core this process may run on (its affinity: all the node's
     CPUs the lease gives it, not the lease's OMP_NUM_THREADS share), timed on
     a render of the same seeded scene at a size chosen for ~target_s seconds
-    (a `sample` x `sample` probe first sets the rate; at most the config's
-    own image).  A reported baseline, not the product (the product path has
-    no CPU fallback)."""
+    (sized_run; at most sample x sample and the config's own image).  A
+    reported baseline, not the product (the product path has no CPU
+    fallback)."""
     from rtamd import scenes as gen
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_py import OracleScene
@@ -153,13 +169,7 @@ def cpu_port_baseline(config: str, sample: int, target_s: float = 10.0, threads:
         dt = time.perf_counter() - t0
         return sum(cnt[k] for k in ("primary", "shadow", "refraction", "reflection")), dt
 
-    r, dt = run(sample)
-    full = gen.CONFIGS[config]["w"]
-    side = int(min(full, sample * (target_s / max(dt, 1e-3)) ** 0.5)) // 64 * 64
-    if side > sample:
-        r, dt = run(side)
-    else:
-        side = sample
+    r, dt, side = sized_run(run, target_s, min(sample, gen.CONFIGS[config]["w"]))
     return {"value": r / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port", "host": host,
             "sample": f"{config} scene at {side}x{side} (full field of view), {r} rays, {dt:.1f} s, "
                       f"C restatement (oracle/rt_oracle.c), OpenMP over rows on {threads} threads"
@@ -446,11 +456,11 @@ def main() -> None:
                 # the lease's OMP_NUM_THREADS share is smaller, that share too:
                 # a lease whose cgroup gives it the time of only some of the CPUs
                 # it sees runs the oversubscribed affinity count slower
-                cpu_port = cpu_port_baseline(args.config, 2 * args.cpu_sample)
+                cpu_port = cpu_port_baseline(args.config, 8 * args.cpu_sample)
                 h = cpu_port["host"]
                 share = h["omp_num_threads"] or (int(h["cgroup_cpus"]) if h["cgroup_cpus"] else 0)
                 if 0 < share < h["affinity"]:
-                    cpu_port["at_lease_share"] = cpu_port_baseline(args.config, 2 * args.cpu_sample,
+                    cpu_port["at_lease_share"] = cpu_port_baseline(args.config, 8 * args.cpu_sample,
                                                                    threads=share)
                     cpu_port["note"] = ("value/cores: all affinity CPUs; at_lease_share: the lease's "
                                         "OMP_NUM_THREADS share (faster when the cgroup quota is that share)")
@@ -518,7 +528,8 @@ def main() -> None:
                                  "achieved_GBps": round(alg_bytes / k_s / 1e9, 3),
                                  "peak_GBps": PEAK_HBM_GBPS,
                                  "frac": round(alg_bytes / k_s / 1e9 / PEAK_HBM_GBPS, 7)}},
-            "cpu_baseline": cpu,
+            # (without oracle/_ref's reference binary: the port, kind "port")
+            "cpu_baseline": cpu if cpu is not None else cpu_port,
             "cpu_port": cpu_port,
             "verified": verified_rows,
             "verified_note": "every rank's rows of the last timed frame (render_kernel without counters) equal "
