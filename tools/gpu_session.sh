@@ -25,7 +25,7 @@ for step in "$@"; do
         > "$out/ab_$a.txt" 2>&1 || { tail -20 "$out/ab_$a.txt"; exit 1; } ;;
     prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof_$a" \
-        -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --config "$a" --steps 10 --warmup 2 --inflight 1 \
+        -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config "$a" --steps 10 --warmup 2 --inflight 1 \
         --cpu-baseline off) > "$out/prof_$a.log" 2>&1 || { tail -20 "$out/prof_$a.log"; exit 1; } ;;
     pmc)
       # FETCH / WRITE bytes and the SQ/TA/TCC counters of one frame, one
