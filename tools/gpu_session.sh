@@ -56,7 +56,9 @@ for step in "$@"; do
       timeout -k 10 600 python -u tools/rank_balance.py "$a" --ns "${b:-1,8}" > "$out/${a}_row_balance.txt" 2>&1 \
         || { tail -20 "$out/${a}_row_balance.txt"; exit 1; } ;;
     cmd)
-      # an arbitrary command line (a = its log name), e.g. cmd:x:'python tools/foo.py'
+      # an arbitrary command line (a = its log name), e.g. cmd:x:'python tools/foo.py';
+      # the command keeps its own colons (pytest -p no:cacheprovider)
+      rest=${step#cmd:}; a=${rest%%:*}; b=${rest#*:}
       timeout -k 10 600 bash -c "$b" > "$out/$a.log" 2>&1 || { tail -20 "$out/$a.log"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
