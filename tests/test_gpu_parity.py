@@ -452,6 +452,39 @@ def test_frames_in_flight(inflight, share):
             gs.set_option("frame_share", bad)
 
 
+def test_frame_share_grid_policy():
+    """Option frame_share's automatic rule (rt_scene.cpp launch_one): with
+    frames in flight, a render of at most 32 pixels per lane of the
+    occupancy-sized grid -- a rank's rows at N >= 2 -- runs on half the grid;
+    a single render in flight, a whole 4096 x 4096 frame (51 per lane), an
+    explicit frame_share 1 and an explicit grid keep theirs.  The image never
+    changes."""
+    hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
+    hs.set_depth(4)
+
+    def grid_of(W, H, **opts):
+        hs.set_imsize(W, H)
+        cam = hs.camera(W, H)
+        gs = rtamd.GpuScene(hs)
+        gs.set_option("counters", 0)
+        for k, v in opts.items():
+            gs.set_option(k, v)
+        img, _ = gs.render_rows(cam, W, H, 0, H)
+        dbg = gs.debug_counters()
+        gs.close()
+        return int(dbg[18]), int(dbg[17]) * int(dbg[23]), img
+    g1, full, ref = grid_of(1024, 512)                       # 0.5 M pixels, one render in flight
+    assert g1 == full
+    g2, _, img = grid_of(1024, 512, inflight=2)
+    assert g2 == full // 2, (g2, full)
+    assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9))
+    assert grid_of(1024, 512, inflight=2, frame_share=1)[0] == full
+    assert grid_of(1024, 512, inflight=2, frame_share=4)[0] == full // 4
+    assert grid_of(1024, 512, inflight=2, grid=100)[0] == 100
+    assert grid_of(4096, 4096, inflight=2)[0] == full       # 51 pixels per lane: the whole grid
+    _summary["frame_share_grids"] = dict(full=full, share2=g2)
+
+
 def test_abi_errors():
     L = rtamd.hip_lib()
     import ctypes as C
