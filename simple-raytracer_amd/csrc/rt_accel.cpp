@@ -21,8 +21,139 @@ double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std
 // Binary SAH tree over P, collapsed into 4-wide nodes (collapse 0: greedy,
 // largest child area first; 1: SAH-optimal) and renumbered breadth-first
 // (the top levels first: cache locality of the hot nodes).
+// SAH cost of a collapsed tree per ray that enters its root, in sphere tests:
+// node_cost per node entered plus the leaves' primitive costs, each weighted
+// by its box's surface area over the root's (a diagnostic: AccelTree::sah).
+double sah_of(const rtbvh::Result4 &Q, const std::vector<float> &costs, double node_cost) {
+    if (Q.nodes.empty()) return 0.0;
+    auto child = [](const rtbvh::Node4 &n, int i) {
+        rtbvh::Box b;
+        for (int k = 0; k < 3; k++) b.lo[k] = n.lo[k][i], b.hi[k] = n.hi[k][i];
+        return b;
+    };
+    rtbvh::Box root;
+    for (int i = 0; i < 4; i++)
+        if (Q.nodes[0].link[i] != rtbvh::kEmpty) root.grow(child(Q.nodes[0], i));
+    const double a0 = root.area();
+    if (!(a0 > 0.0) || !std::isfinite(a0)) return 0.0;
+    double c = node_cost;
+    for (const auto &n : Q.nodes)
+        for (int i = 0; i < 4; i++) {
+            const int32_t l = n.link[i];
+            if (l == rtbvh::kEmpty) continue;
+            const double a = child(n, i).area() / a0;
+            if (l >= 0) {
+                c += node_cost * a;
+            } else {
+                const int v = -l - 1, first = v >> 4, count = v & 15;
+                double w = 0.0;
+                for (int q = 0; q < count; q++) w += costs[(size_t)first + q];
+                c += a * w;
+            }
+        }
+    return c;
+}
+
+// Pre-splitting (AccelOpts::presplit, after Ernst and Greiner's early split
+// clipping): a face whose box is much larger than the face -- a thin or
+// slanted triangle -- becomes several references, each with the box of the
+// part of the triangle inside one piece of its box (the largest piece split
+// at the middle of its longest axis, the triangle clipped to each half in
+// double), so that the tree's boxes overlap less.  Exact: every point of the
+// triangle lies in some piece's box, each piece padded as the whole face is
+// (build_accel), so a ray that meets the face enters a leaf holding it; a
+// leaf tests a face once however many of its references it holds
+// (leaf_records), and a ray visiting two leaves of one face meets the same
+// candidate twice -- the same closest hit, and the same answer for an any-hit
+// search when the face's shadow factor is 0 or 1 (x 0 twice is x 0, x 1 is
+// exact).  Faces with any other factor (translucent: a duplicate would
+// multiply twice) keep one reference.
+struct ClipBox {
+    double lo[3], hi[3];
+    double area() const {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+// the box of the triangle's part inside [blo, bhi] (false: none)
+bool clip_box(const float v[3][3], const double blo[3], const double bhi[3], ClipBox &out) {
+    double poly[12][3], tmp[12][3];
+    int n = 3;
+    for (int i = 0; i < 3; i++)
+        for (int k = 0; k < 3; k++) poly[i][k] = v[i][k];
+    for (int ax = 0; ax < 3 && n > 0; ax++)
+        for (int side = 0; side < 2 && n > 0; side++) {
+            const double s = side == 0 ? blo[ax] : bhi[ax];
+            auto inside = [&](const double *p) { return side == 0 ? p[ax] >= s : p[ax] <= s; };
+            int m = 0;
+            for (int i = 0; i < n; i++) {
+                const double *a = poly[i], *b = poly[(i + 1) % n];
+                const bool ia = inside(a), ib = inside(b);
+                if (ia) {
+                    for (int k = 0; k < 3; k++) tmp[m][k] = a[k];
+                    m++;
+                }
+                if (ia != ib) {
+                    const double t = (s - a[ax]) / (b[ax] - a[ax]);
+                    for (int k = 0; k < 3; k++) tmp[m][k] = a[k] + t * (b[k] - a[k]);
+                    tmp[m][ax] = s;
+                    m++;
+                }
+            }
+            n = m;
+            for (int i = 0; i < n; i++)
+                for (int k = 0; k < 3; k++) poly[i][k] = tmp[i][k];
+        }
+    if (n == 0) return false;
+    for (int k = 0; k < 3; k++) out.lo[k] = INFINITY, out.hi[k] = -INFINITY;
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++)
+            out.lo[k] = std::min(out.lo[k], std::max(poly[i][k], blo[k])),
+            out.hi[k] = std::max(out.hi[k], std::min(poly[i][k], bhi[k]));
+    return true;
+}
+// a face's pieces (at most max_refs; one when splitting does not pay): the
+// largest piece is split while its halves' boxes have at most kPresplitGain
+// of its box's area (host SAH over C3 / C4 at 0.5 ... 0.9: 0.9 lowest)
+void split_face(const float v[3][3], int max_refs, std::vector<ClipBox> &pieces) {
+    pieces.clear();
+    ClipBox whole;
+    for (int k = 0; k < 3; k++) {
+        whole.lo[k] = std::min((double)v[0][k], std::min((double)v[1][k], (double)v[2][k]));
+        whole.hi[k] = std::max((double)v[0][k], std::max((double)v[1][k], (double)v[2][k]));
+    }
+    pieces.push_back(whole);
+    std::vector<bool> done(1, false);
+    while ((int)pieces.size() < max_refs) {
+        int best = -1;
+        for (int i = 0; i < (int)pieces.size(); i++)
+            if (!done[i] && (best < 0 || pieces[i].area() > pieces[best].area())) best = i;
+        if (best < 0) break;
+        const ClipBox b = pieces[best];
+        int ax = 0;
+        for (int k = 1; k < 3; k++)
+            if (b.hi[k] - b.lo[k] > b.hi[ax] - b.lo[ax]) ax = k;
+        const double mid = 0.5 * (b.lo[ax] + b.hi[ax]);
+        double llo[3], lhi[3], rlo[3], rhi[3];
+        for (int k = 0; k < 3; k++) llo[k] = rlo[k] = b.lo[k], lhi[k] = rhi[k] = b.hi[k];
+        lhi[ax] = mid;
+        rlo[ax] = mid;
+        ClipBox L, R;
+        const bool hl = clip_box(v, llo, lhi, L), hr = clip_box(v, rlo, rhi, R);
+        // split only where the two pieces' boxes cover clearly less than the
+        // piece did (a compact piece stays whole)
+        if (!hl || !hr || L.area() + R.area() > kPresplitGain * b.area()) {
+            done[best] = true;
+            continue;
+        }
+        pieces[best] = L;
+        pieces.push_back(R);
+        done.push_back(false);
+    }
+}
+
 bool build_wide(const AccelOpts &o, int threads, std::vector<rtbvh::Prim> &P, rtbvh::Result &R, rtbvh::Result4 &Q,
-                double *ms) {
+                double *ms, double *sah = nullptr) {
     auto t0 = Clock::now();
     rtbvh::Builder B(P);
     B.max_leaf = o.collapse ? 1 : o.bvh_leaf;
@@ -37,6 +168,7 @@ bool build_wide(const AccelOpts &o, int threads, std::vector<rtbvh::Prim> &P, rt
         rtbvh::collapse<4>(R, Q);
     rtbvh::bfs_order(Q);
     if (ms) ms[2] += ms_since(t0);
+    if (sah) *sah = sah_of(Q, R.costs, (double)o.node_milli / 1000.0);
     return true;
 }
 
@@ -221,6 +353,8 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in) {
         float4 a = in.fscan[5 * i + 1], b2 = in.fscan[5 * i + 2], c2 = in.fscan[5 * i + 3];
         double det = a.w, d11 = b2.w, d22 = c2.w;
         ps.cond = det > 0 ? d11 * d22 / det : 1e30;
+        for (int j = 0; j < 3; j++)
+            for (int k = 0; k < 3; k++) ps.v[j][k] = F.v[j][k];
         in.prims.push_back(ps);
     }
     in.sscan.assign((size_t)ns, make_float4(0, 0, 0, 0));
@@ -270,6 +404,7 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in) {
         V3 c = vcross(f3(&in.fscan[5 * i + 2].x), f3(&in.fscan[5 * i + 3].x));
         xs += 0.25 * std::sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z);
     }
+    const double xf = xs;
     for (int i = 0; i < ns; i++) xs += kPi * (double)in.sscan[i].w * (double)in.sscan[i].w;
     for (int k = 0; k < 3; k++) {
         const double e = (double)in.scene_hi[k] - (double)in.scene_lo[k];
@@ -277,6 +412,7 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in) {
         diag2 += e * e;
     }
     in.crossings = vol > 0.0 && std::isfinite(xs) ? xs / vol * std::sqrt(diag2) : 0.0;
+    in.face_crossings = vol > 0.0 && std::isfinite(xf) ? xf / vol * std::sqrt(diag2) : 0.0;
 }
 
 double distance_bound(const AccelInput &in, const float eye[3]) {
@@ -332,10 +468,46 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
         }
       }
     });
+    // automatic: 2 references per face where faces alone are dense (a line
+    // across the scene meets >= kPresplitDensity of them: C4 6.5 -> +5.6 %;
+    // C3's 0.7 -> -1.0 %, its box tests +4 %, profiles/r05/ab/presplit_*.txt)
+    const int presplit = o.presplit >= 0 ? o.presplit : (in.face_crossings >= kPresplitDensity ? kPresplitAuto : 0);
+    out.presplit = presplit;
+    if (presplit > 1) {
+        // faces with a shadow factor of exactly 0 or 1 and finite boxes: their
+        // pieces (split_face), in primitive order (the same tree for every
+        // thread count)
+        std::vector<rtbvh::Prim> S;
+        S.reserve(P.size());
+        std::vector<ClipBox> pieces;
+        for (size_t i = 0; i < P.size(); i++) {
+            const auto &src = in.prims[i];
+            const float fac = src.sphere ? 0.5f : in.ofac[(size_t)src.key];
+            bool finite = true;
+            for (int k = 0; k < 3; k++) finite &= std::isfinite(P[i].box.lo[k]) && std::isfinite(P[i].box.hi[k]);
+            if (src.sphere || !finite || !(fac == 0.0f || fac == 1.0f)) {
+                S.push_back(P[i]);
+                continue;
+            }
+            split_face(src.v, presplit, pieces);
+            const double pad = std::ldexp(D, -16) * std::max(1.0, src.cond);
+            for (const ClipBox &c : pieces) {
+                rtbvh::Prim q = P[i];
+                for (int k = 0; k < 3; k++) {
+                    q.box.lo[k] = std::nextafter((float)(c.lo[k] - pad), -INFINITY);
+                    q.box.hi[k] = std::nextafter((float)(c.hi[k] + pad), INFINITY);
+                    q.c[k] = (float)(0.5 * (c.lo[k] + c.hi[k]));
+                }
+                S.push_back(q);
+            }
+        }
+        P.swap(S);
+    }
+    out.refs = (long long)P.size();
     out.ms[0] = ms_since(t0);
     rtbvh::Result R;
     rtbvh::Result4 Q;
-    bool ok = P.empty() || build_wide(o, threads, P, R, Q, out.ms);
+    bool ok = P.empty() || build_wide(o, threads, P, R, Q, out.ms, &out.sah);
     // leaf records: face = its 5 scan words with (key, shadow factor) in the
     // last one's y, z; sphere = (centre, r), (key, shadow factor, 0, 0)
     t0 = Clock::now();

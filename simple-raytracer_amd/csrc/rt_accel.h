@@ -28,6 +28,7 @@ struct PrimSrc {
     float lo[3], hi[3];                // face: vertex bounds; sphere: centre +- r
     float c[3], r;                     // sphere centre / radius
     double cond;                       // face: |e1|^2 |e2|^2 / det
+    float v[3][3];                     // face: its vertices (AccelOpts::presplit clips the triangle)
 };
 
 // Everything the device scene store holds, built on the host from the scene
@@ -46,6 +47,7 @@ struct AccelInput {
     bool secondary = false;            // some material reflects or refracts
     bool nan_fac = false;              // some shadow factor is NaN (no opaque early exit)
     double crossings = 0.0;            // objects a line across the scene meets on average
+    double face_crossings = 0.0;       // ... faces only (AccelOpts::presplit's automatic value)
 };
 
 // rt_scene_desc -> the host arrays (exact per-face invariants, main.cpp:1280-1301)
@@ -55,12 +57,17 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in);
 // scene's bounds) to any primitive: the BVH padding's scale.
 double distance_bound(const AccelInput &in, const float eye[3]);
 
+constexpr double kPresplitDensity = 2.0;   // face crossings from which faces are pre-split (AccelOpts)
+constexpr int kPresplitAuto = 2;           // ... into at most this many references each
+constexpr double kPresplitGain = 0.9;      // a piece is split when its halves' boxes have <= this of its area
 struct AccelOpts {
     int bvh_leaf = 8;                  // leaf size limit of the collapse
     int collapse = 1;                  // binary -> 4-wide: 0 greedy, 1 SAH-optimal
     int node_milli = 500;              // SAH collapse: node visit cost, x1000 of a sphere test
     int threads = 0;                   // host threads for the build (0: automatic, 1: serial)
     int hot_copies = 0;                // copies of the main tree's top nodes (0/1: none; else a power of 2)
+    int presplit = -1;                 // references per face at most (0/1: one; -1: kPresplitAuto in scenes
+                                       // of dense faces; build_accel's presplit)
 };
 
 // Copies of the top of the main tree (its first kHotNodes nodes in BFS order,
@@ -83,6 +90,9 @@ struct AccelTree {
     int depth = 0, max_stack = 0;      // main tree
     int stack_all = 0;                 // deepest worst-case stack over all trees
     long long main_nodes = 0;
+    long long refs = 0;                // primitive references in the main tree (> objects with presplit)
+    int presplit = 0;                  // references per face at most, as built
+    double sah = 0.0;                  // the main tree's SAH cost (node visits + primitive tests per ray, rt_accel.cpp)
     int threads = 1;                   // host threads used
     // hot copies (AccelOpts::hot_copies): copy c's root at byte offset
     // hot_base + c * hot_stride of the node buffer; hot_nodes holds the copies

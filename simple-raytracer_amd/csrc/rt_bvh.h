@@ -647,15 +647,20 @@ inline bool leaf_records(ResultW<W> &Q, const std::vector<int32_t> &keys, IsFace
             int v = -l - 1, first = v >> 4, count = v & 15;
             // faces first, each kind in key order (a stable insertion sort:
             // count <= 15)
+            // (a primitive with several references in the leaf -- build_accel's
+            // presplit -- is recorded once)
             int32_t ks[16];
             bool fs[16];
+            int m = 0;
             for (int q = 0; q < count; q++) {
                 const int32_t k = keys[(size_t)first + q];
+                if (std::find(ks, ks + m, k) != ks + m) continue;
                 const bool f = is_face(k);
-                int w = q;
+                int w = m++;
                 while (w > 0 && (fs[w - 1] != f ? f : k < ks[w - 1])) ks[w] = ks[w - 1], fs[w] = fs[w - 1], w--;
                 ks[w] = k, fs[w] = f;
             }
+            count = m;
             int nfaces = 0;
             for (int q = 0; q < count; q++) nfaces += fs[q] ? 1 : 0;
             // off <= 2^23 - 2 keeps every link above INT_MIN + 256 (device sentinels)

@@ -876,6 +876,39 @@ def test_refill_options_bit_identical():
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
 
+@pytest.mark.parametrize("name,size", [("C3_64x64.txt", None), ("C4_32x32.txt", None), ("test7_s.txt", (37, 23)),
+                                       ("house_s.txt", None), ("edge_glass_faces.txt", None),
+                                       ("earth_pyramid_s.txt", None)])
+def test_bvh_presplit_bit_identical(name, size):
+    """Option bvh_presplit: faces with a shadow factor of 0 or 1 enter the BVH
+    as several references with clipped boxes (rt_accel.cpp presplit;
+    automatically 2 in scenes of dense faces -- C4 -- else none).  Every
+    point of a face stays inside some reference's padded box, a leaf records
+    a face once, and a face met twice answers the same: images and per-type
+    ray counts bit for bit against the unsplit tree (and the unsplit image
+    against the oracle's); the tree did change where faces were split."""
+    kw = dict(cwd=SCENES, imsize=size)
+    ref, st = rtamd.render_scene(name, options={"accel": 1, "bvh_presplit": 0}, **kw)
+    changed = False
+    for ps in (-1, 2, 4):                       # (-1: automatic -- 2 for C4's dense faces, else 0)
+        img, st2 = rtamd.render_scene(name, options={"accel": 1, "bvh_presplit": ps}, **kw)
+        assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, ps)
+        assert _counts(st2) == _counts(st), (name, ps)
+        changed |= st2.box_tests != st.box_tests
+    auto, st_a = rtamd.render_scene(name, options={"accel": 1}, **kw)
+    if name == "C4_32x32.txt":
+        _, st_2 = rtamd.render_scene(name, options={"accel": 1, "bvh_presplit": 2}, **kw)
+        assert st_a.box_tests == st_2.box_tests != st.box_tests
+    elif name == "C3_64x64.txt":
+        assert st_a.box_tests == st.box_tests
+    if name in ("C3_64x64.txt", "C4_32x32.txt"):
+        assert changed
+        o, _ = OracleScene(name, cwd=SCENES).render(*(size or ()))
+        assert_parity(ref, o, f"{name} presplit")
+    with pytest.raises(rtamd.RTError):
+        rtamd.render_scene(name, options={"bvh_presplit": 9}, **kw)
+
+
 def test_last_light_skip_and_recursive_instantiation_bit_identical():
     """Scenes without reflecting or refracting materials render with the
     MAXF = 1 instantiation, which counts a last light's shadow ray whose Phong
