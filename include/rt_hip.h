@@ -255,6 +255,9 @@ int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *
  * "org_first" (-1 auto, or bits 1 shadow / 2 refraction / 4 reflection rays:
  * test the ray's origin object's BVH leaf before the search from the root;
  * auto = 6 in dense scenes, else 0 -- never changes the image),
+ * "bvh_presplit" (0..8, default 0: faces whose shadow factor is 0 or 1 enter
+ * the BVH as up to that many references with clipped boxes -- never changes
+ * the image; measured per scene, not a default),
  * "hot_copies" (0, or a power of 2 up to 64: copies of the main BVH's top
  * 64 nodes and their leaves, each wave starting its searches in one of them --
  * spreads the reads every search makes of the root over L2 channels; never

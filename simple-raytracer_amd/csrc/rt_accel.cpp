@@ -404,7 +404,6 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in) {
         V3 c = vcross(f3(&in.fscan[5 * i + 2].x), f3(&in.fscan[5 * i + 3].x));
         xs += 0.25 * std::sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z);
     }
-    const double xf = xs;
     for (int i = 0; i < ns; i++) xs += kPi * (double)in.sscan[i].w * (double)in.sscan[i].w;
     for (int k = 0; k < 3; k++) {
         const double e = (double)in.scene_hi[k] - (double)in.scene_lo[k];
@@ -412,7 +411,6 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in) {
         diag2 += e * e;
     }
     in.crossings = vol > 0.0 && std::isfinite(xs) ? xs / vol * std::sqrt(diag2) : 0.0;
-    in.face_crossings = vol > 0.0 && std::isfinite(xf) ? xf / vol * std::sqrt(diag2) : 0.0;
 }
 
 double distance_bound(const AccelInput &in, const float eye[3]) {
@@ -468,10 +466,12 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
         }
       }
     });
-    // automatic: 2 references per face where faces alone are dense (a line
-    // across the scene meets >= kPresplitDensity of them: C4 6.5 -> +5.6 %;
-    // C3's 0.7 -> -1.0 %, its box tests +4 %, profiles/r05/ab/presplit_*.txt)
-    const int presplit = o.presplit >= 0 ? o.presplit : (in.face_crossings >= kPresplitDensity ? kPresplitAuto : 0);
+    // (off by default: 2 references per face took the benchmark's C4 from
+    // 14.11 to 13.36 ms, but four other seeds of its generator -2.8 ... +5.1 %,
+    // and C3 -1.0 %; a split-gain of 0.8 or 0.95 instead of 0.9 lost on C4
+    // itself -- the tree's response is not a property of the scene kind,
+    // profiles/r05/ab/presplit_*)
+    const int presplit = std::max(0, o.presplit);
     out.presplit = presplit;
     if (presplit > 1) {
         // faces with a shadow factor of exactly 0 or 1 and finite boxes: their

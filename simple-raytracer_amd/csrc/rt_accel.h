@@ -47,7 +47,6 @@ struct AccelInput {
     bool secondary = false;            // some material reflects or refracts
     bool nan_fac = false;              // some shadow factor is NaN (no opaque early exit)
     double crossings = 0.0;            // objects a line across the scene meets on average
-    double face_crossings = 0.0;       // ... faces only (AccelOpts::presplit's automatic value)
 };
 
 // rt_scene_desc -> the host arrays (exact per-face invariants, main.cpp:1280-1301)
@@ -57,17 +56,17 @@ void accel_input(const rt_scene_desc *desc, AccelInput &in);
 // scene's bounds) to any primitive: the BVH padding's scale.
 double distance_bound(const AccelInput &in, const float eye[3]);
 
-constexpr double kPresplitDensity = 2.0;   // face crossings from which faces are pre-split (AccelOpts)
-constexpr int kPresplitAuto = 2;           // ... into at most this many references each
-constexpr double kPresplitGain = 0.9;      // a piece is split when its halves' boxes have <= this of its area
+#ifndef RT_PRESPLIT_GAIN
+#define RT_PRESPLIT_GAIN 0.9
+#endif
+constexpr double kPresplitGain = RT_PRESPLIT_GAIN;   // a piece is split when its halves' boxes have <= this of its area
 struct AccelOpts {
     int bvh_leaf = 8;                  // leaf size limit of the collapse
     int collapse = 1;                  // binary -> 4-wide: 0 greedy, 1 SAH-optimal
     int node_milli = 500;              // SAH collapse: node visit cost, x1000 of a sphere test
     int threads = 0;                   // host threads for the build (0: automatic, 1: serial)
     int hot_copies = 0;                // copies of the main tree's top nodes (0/1: none; else a power of 2)
-    int presplit = -1;                 // references per face at most (0/1: one; -1: kPresplitAuto in scenes
-                                       // of dense faces; build_accel's presplit)
+    int presplit = 0;                  // references per face at most (0/1: one; build_accel's presplit)
 };
 
 // Copies of the top of the main tree (its first kHotNodes nodes in BFS order,

@@ -70,7 +70,7 @@ struct rt_scene {
     long long opt_reserve = 0;         // occupancy-derived grid: block slots left free for other kernels
     long long opt_accel = -1;          // -1 auto, 0 brute-force scan, 1 BVH
     long long opt_bvh_leaf = 8;        // SAH max leaf size
-    long long opt_bvh_presplit = -1;   // references per opaque face at most (rt_accel.cpp presplit; -1 auto)
+    long long opt_bvh_presplit = 0;    // references per opaque face at most (rt_accel.cpp presplit)
     long long opt_bvh_collapse = 1;    // binary -> 4-wide: 0 greedy (largest area first), 1 SAH-optimal DP
     long long opt_bvh_node = 500;      // DP collapse: cost of a 4-wide node visit, x1000 of a sphere test
                                        // (A/B, C3: 0.25 / 0.5 / 0.75 / 1 / 2 -> +0.6 / +0.5 / +0.5 / +0.2 / -1.7 %)
@@ -733,7 +733,7 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         s->opt_lds_stack = value;
     }
     else if (k == "bvh_presplit") {
-        if (value < -1 || value > 8) return RT_E_INVALID;
+        if (value < 0 || value > 8) return RT_E_INVALID;
         s->opt_bvh_presplit = value;
         s->bvh_D = -1.0;               // rebuild on the next render
     }

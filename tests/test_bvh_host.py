@@ -51,11 +51,9 @@ def test_bvh_device_padding_stack(checker):
 # the round-4 builder (primitive array reordered in place, one-pass range
 # statistics, sparse bins for small ranges, subtrees on threads, bitwise
 # binary16 rounding) builds the same trees.  64: the same trees stored as the
-# round-5 64-B nodes with 8-bit planes (build option RT_NODE8=1).  C4's trees
-# since round 5: its faces pre-split into up to 2 references each (dense
-# faces, rt_accel.cpp presplit).
-BENCH_TREE_HASH = {104: {"C3": "d0d4c36f4057bc62", "C4": "2c67e3453aa82439", "C5": "0fa041b2ecb60269"},
-                   64: {"C3": "04afc4732a2a9f6b", "C4": "fa293dfa1c95ce99", "C5": "c6ebbeb0f0baad7c"}}
+# round-5 64-B nodes with 8-bit planes (build option RT_NODE8=1).
+BENCH_TREE_HASH = {104: {"C3": "d0d4c36f4057bc62", "C4": "5023c92e900cccd1", "C5": "0fa041b2ecb60269"},
+                   64: {"C3": "04afc4732a2a9f6b", "C4": "a76af2eedeb8ab63", "C5": "c6ebbeb0f0baad7c"}}
 
 
 @pytest.fixture(scope="module")

@@ -881,8 +881,8 @@ def test_refill_options_bit_identical():
                                        ("earth_pyramid_s.txt", None)])
 def test_bvh_presplit_bit_identical(name, size):
     """Option bvh_presplit: faces with a shadow factor of 0 or 1 enter the BVH
-    as several references with clipped boxes (rt_accel.cpp presplit;
-    automatically 2 in scenes of dense faces -- C4 -- else none).  Every
+    as several references with clipped boxes (rt_accel.cpp presplit; off by
+    default).  Every
     point of a face stays inside some reference's padded box, a leaf records
     a face once, and a face met twice answers the same: images and per-type
     ray counts bit for bit against the unsplit tree (and the unsplit image
@@ -890,17 +890,13 @@ def test_bvh_presplit_bit_identical(name, size):
     kw = dict(cwd=SCENES, imsize=size)
     ref, st = rtamd.render_scene(name, options={"accel": 1, "bvh_presplit": 0}, **kw)
     changed = False
-    for ps in (-1, 2, 4):                       # (-1: automatic -- 2 for C4's dense faces, else 0)
+    for ps in (2, 4):
         img, st2 = rtamd.render_scene(name, options={"accel": 1, "bvh_presplit": ps}, **kw)
         assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), (name, ps)
         assert _counts(st2) == _counts(st), (name, ps)
         changed |= st2.box_tests != st.box_tests
-    auto, st_a = rtamd.render_scene(name, options={"accel": 1}, **kw)
-    if name == "C4_32x32.txt":
-        _, st_2 = rtamd.render_scene(name, options={"accel": 1, "bvh_presplit": 2}, **kw)
-        assert st_a.box_tests == st_2.box_tests != st.box_tests
-    elif name == "C3_64x64.txt":
-        assert st_a.box_tests == st.box_tests
+    _, st_d = rtamd.render_scene(name, options={"accel": 1}, **kw)
+    assert st_d.box_tests == st.box_tests          # (off by default)
     if name in ("C3_64x64.txt", "C4_32x32.txt"):
         assert changed
         o, _ = OracleScene(name, cwd=SCENES).render(*(size or ()))

@@ -128,7 +128,7 @@ int main(int argc, char **argv) {
     accel_input(desc, in);
     const double input_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
     const double D = distance_bound(in, cam.eye);
-    const int presplit = argc > 5 ? std::atoi(argv[5]) : -1;   // -1: automatic (as rt_scene builds it)
+    const int presplit = argc > 5 ? std::atoi(argv[5]) : 0;
     AccelTree ref, par;
     double best[2] = {1e30, 1e30}, ph[2][6];
     for (int r = 0; r < reps; r++) {
