@@ -235,7 +235,7 @@ int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *
  * 2 with inflight > 1 for a render with at most 32 pixels per lane of the
  * occupancy-sized grid -- C3's rows of one rank at N >= 2 --, else 1; ignored when
  * "grid" is set -- never changes the image),
- * "lds_stack" (12..16, default 14: BVH stack entries kept in LDS per lane;
+ * "lds_stack" (12..16, default 15: BVH stack entries kept in LDS per lane;
  * deeper stacks spill to device memory -- a test knob), "bvh_leaf" (largest
  * leaf), "bvh_collapse" (0 greedy, 1 SAH-optimal 4-wide collapse), "bvh_node"
  * (the collapse's node cost x1000), "bvh_threads" (host threads of the BVH

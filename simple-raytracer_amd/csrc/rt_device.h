@@ -162,14 +162,15 @@ constexpr int kStackMax = 512;
 // deeper stack spills its oldest kSpill entries to device memory (rare)
 constexpr int kLdsStack = 16;            // most entries the LDS share may hold (option lds_stack)
 #ifndef RT_LDS_STACK
-#define RT_LDS_STACK 14                  // 16 (32 KB per block with the shading state): 5 blocks per CU
-                                         // on paper, -8.6 % measured; 14: 270 spills per C3 frame
+#define RT_LDS_STACK 15                  // 16 (32 KB per block with the shading state): 5 blocks per CU
+                                         // on paper, -8.6 % measured; 15 (31.8 KB): C3 +-0, C4 +0.5 %
+                                         // against 14 (profiles/r05/ab/lds_stack15_*.txt)
 #endif
 constexpr int kLdsStackDefault = RT_LDS_STACK;
 #ifndef RT_LDS_STACK_DEEP
-#define RT_LDS_STACK_DEEP 14             // depth > 4 (render_kernel<9 / 17, *>): 16 entries with the
+#define RT_LDS_STACK_DEEP 15             // depth > 4 (render_kernel<9 / 17, *>): 16 entries with the
                                          // lights in device memory (32 KB per block) cost C5 8.5 %
-                                         // (profiles/r03/ab_deep_stack.txt)
+                                         // (profiles/r03/ab_deep_stack.txt), 15 gains 0.55 % on C5 (r05)
 #endif
 constexpr int kLdsStackDeep = RT_LDS_STACK_DEEP;
 #ifndef RT_SPILL

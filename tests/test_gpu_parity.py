@@ -838,7 +838,7 @@ def test_lds_stack_spill():
         cam = hs.camera()
         ref, st = rtamd.GpuScene(hs).render_rows(cam, W, H, 0, H)
         gs = rtamd.GpuScene(hs)
-        gs.set_option("lds_stack", 12)    # default 14
+        gs.set_option("lds_stack", 12)    # default 15
         img, st2 = gs.render_rows(cam, W, H, 0, H)
         assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(ref, nan=-9)), name
         assert _counts(st2) == _counts(st)
