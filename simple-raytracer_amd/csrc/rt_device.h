@@ -99,6 +99,10 @@ struct Params {
     const float4 *__restrict__ sscan;
     const float *__restrict__ ofac;      // (float)(1.0 - opacity) per object (main.cpp:909)
     const ObjK *__restrict__ objs;
+#if RT_PROBE
+    const ObjK *objs2;                   // (traffic probe builds: copies of objs / sscan read beside them)
+    const float4 *sscan2;
+#endif
     const FaceShadeK *__restrict__ fsh;
     const LightK *__restrict__ lights;
     const unsigned char *__restrict__ texels;   // all textures: RGB bytes, row-major
@@ -191,6 +195,10 @@ constexpr long long kFrameShare = RT_FRAME_SHARE;
 #define RT_FRAME_SHARE_ITEMS 32          // ... for frames of at most this many work items per lane of the grid
 #endif
 constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
+#ifndef RT_PROBE
+#define RT_PROBE 0                       // traffic probes (measurement builds only): bit 0 the object record at a
+                                         // node's open, 1 the sphere at a hit, 2 the object record at a light step
+#endif
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

@@ -1022,6 +1022,9 @@ __device__ __forceinline__ HitRec hit_geometry(const Params &p, int obj, V3 o, V
     } else {
         float4 s = row(p.sscan, obj - p.nf);
         h.N = vnorm(vdiv(vsub(h.P, V3{s.x, s.y, s.z}), s.w));
+#if RT_PROBE & 2
+        if (row(p.sscan2, obj - p.nf).w == -12345.0f) h.N.x = 0.0f;   // traffic probe (never true)
+#endif
     }
     return h;
 }
@@ -1118,6 +1121,12 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
     const HitRec hr = hit_geometry(p, obj, o, d, t);
     V3 N = hr.N;
     const ObjK &ob = row(p.objs, obj);
+#if RT_PROBE & 1
+    {   // traffic probe: the same record's two sectors from a copy (never true)
+        const ObjK &o2 = row(p.objs2, obj);
+        if (o2.tex == -12345 && o2.dif[0] == -12345.0f) N.x = 0.0f;
+    }
+#endif
     V3 I = vmul(d, -1.0f);
     float cosI = vdot(N, I);
     C3 dif = {ob.dif[0], ob.dif[1], ob.dif[2]};
@@ -1368,6 +1377,12 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
             const int light = h_light(h);
             const ObjK &ob = row(p.objs, h.obj);
+#if RT_PROBE & 4
+            {   // traffic probe: the light step's fields from a copy (never true)
+                const ObjK &o2 = row(p.objs2, h.obj);
+                if (o2.spc[0] == -12345.0f && o2.n == -12345.0f) h.acc.r = 0.0f;
+            }
+#endif
             // the light's words in one batch (LightK: xyz w | col | L)
             const LightW lw = light_words(p, light);
             const f4v lw0 = lw.w0, lw1 = lw.w1, lw2 = lw.w2;

@@ -569,6 +569,9 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
         const size_t o_fscan = a.add(in.fscan), o_sscan = a.add(in.sscan), o_ofac = a.add(in.ofac);
         const size_t o_objs = a.add(in.objs), o_fsh = a.add(in.fsh), o_lights = a.add(in.lights);
         const size_t o_texels = a.reserve(tex_bytes), o_texs = a.add(texs);
+#if RT_PROBE
+        const size_t o_objs2 = a.add(in.objs), o_sscan2 = a.add(in.sscan);
+#endif
         for (int i = 0; i < desc->n_textures; i++) {
             const rt_texture_desc &T = desc->textures[i];
             std::memcpy(a.host.data() + o_texels + (size_t)texs[i].off, T.rgb, (size_t)T.width * T.height * 3);
@@ -587,6 +590,10 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
             p.lights = reinterpret_cast<const LightK *>(d + o_lights);
             p.texels = reinterpret_cast<const unsigned char *>(d + o_texels);
             p.texs = reinterpret_cast<const TexK *>(d + o_texs);
+#if RT_PROBE
+            p.objs2 = reinterpret_cast<const ObjK *>(d + o_objs2);
+            p.sscan2 = reinterpret_cast<const float4 *>(d + o_sscan2);
+#endif
         }
     }
     tm.mark("uploads");
