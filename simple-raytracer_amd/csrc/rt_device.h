@@ -102,6 +102,7 @@ struct Params {
 #if RT_PROBE
     const ObjK *objs2;                   // (traffic probe builds: copies of objs / sscan read beside them)
     const float4 *sscan2;
+    void *frames2;                       // (probe bit 3: a second copy of the frame heads, written and read beside them)
 #endif
     const FaceShadeK *__restrict__ fsh;
     const LightK *__restrict__ lights;
@@ -197,7 +198,8 @@ constexpr long long kFrameShare = RT_FRAME_SHARE;
 constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 #ifndef RT_PROBE
 #define RT_PROBE 0                       // traffic probes (measurement builds only): bit 0 the object record at a
-                                         // node's open, 1 the sphere at a hit, 2 the object record at a light step
+                                         // node's open, 1 the sphere at a hit, 2 the object record at a light step,
+                                         // 3 the frame head at a child's open and return
 #endif
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST

@@ -1297,6 +1297,12 @@ struct LaneState {
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         return reinterpret_cast<Cold<MAXF> *>(frames) + ((size_t)blockIdx.x * kBlock + t) * MAXF;
     }
+#if RT_PROBE & 8
+    void *frames2;
+    __device__ __forceinline__ Cold<MAXF> *cold2() const {
+        return reinterpret_cast<Cold<MAXF> *>(frames2) + ((size_t)blockIdx.x * kBlock + threadIdx.x) * MAXF;
+    }
+#endif
 };
 
 __device__ __forceinline__ void shadow_query(Query &q, const Params &p, int light, int self) {
@@ -1467,6 +1473,9 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             // dif.r: F_t (refraction child) or F_r (reflection child)
             if (h_phase(h) == PH_REFR_CHILD) cold_save_ext(c, q.o, h);
             cold_save_head(c, h, h.dif.r);
+#if RT_PROBE & 8
+            cold_save_head(ls.cold2()[top], h, h.dif.r);     // traffic probe: the head again, in a copy
+#endif
             top++;
         }
     }
@@ -1540,6 +1549,12 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
         top--;
         const Cold<MAXF> &pc = ls.cold()[top];
         const float f = cold_restore_head(pc, h);
+#if RT_PROBE & 8
+        {   // traffic probe: the copy's head read back (never true)
+            HotR h2 = h;
+            if (cold_restore_head(ls.cold2()[top], h2) == -12345.0f && h2.meta == 0xdeadbeefu) h.acc.r = 0.0f;
+        }
+#endif
         if (h_phase(h) == PH_REFR_CHILD) {           // main.cpp:1072-1083
             q.o = cold_restore_ext(pc, h);
             h.dif.r = f;                             // F_t
@@ -1621,6 +1636,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     LaneState<MAXF> ls;
     ls.top = -1;
     ls.frames = p.frames;
+#if RT_PROBE & 8
+    ls.frames2 = p.frames2;
+#endif
     CountersT<COUNT> cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;

@@ -263,6 +263,20 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     }
     tm.mark("frames");
     pl.frames = slot.d_frames;
+#if RT_PROBE & 8
+    {   // traffic probe: a second frame area (measurement builds only; kept for the process)
+        static void *f2 = nullptr;
+        static size_t f2_cap = 0;
+        if (f2_cap < cold_bytes) {
+            if (f2) (void)hipFree(f2);
+            f2 = nullptr;
+            f2_cap = 0;
+            if (hipMalloc(&f2, cold_bytes) != hipSuccess) return hipErrorOutOfMemory;
+            f2_cap = cold_bytes;
+        }
+        pl.frames2 = f2;
+    }
+#endif
     pl.ovf = reinterpret_cast<int *>(static_cast<char *>(slot.d_frames) + cold_bytes);
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
