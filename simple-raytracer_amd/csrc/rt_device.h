@@ -102,7 +102,6 @@ struct Params {
 #if RT_PROBE
     const ObjK *objs2;                   // (traffic probe builds: copies of objs / sscan read beside them)
     const float4 *sscan2;
-    void *frames2;                       // (probe bit 3: a second copy of the frame heads, written and read beside them)
 #endif
     const FaceShadeK *__restrict__ fsh;
     const LightK *__restrict__ lights;
@@ -196,10 +195,17 @@ constexpr long long kFrameShare = RT_FRAME_SHARE;
 #define RT_FRAME_SHARE_ITEMS 32          // ... for frames of at most this many work items per lane of the grid
 #endif
 constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
+#ifndef RT_DENSE_HEADS_MIN
+#define RT_DENSE_HEADS_MIN 9             // instantiations with MAXF >= this keep their frame heads in a dense
+                                         // [level][lane] array (rt_kernels.hip Fr): depth > 4
+#endif
+constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
+constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
+constexpr int kHeadStack = 3;            // medium-stack entries in a dense head slot
 #ifndef RT_PROBE
 #define RT_PROBE 0                       // traffic probes (measurement builds only): bit 0 the object record at a
-                                         // node's open, 1 the sphere at a hit, 2 the object record at a light step,
-                                         // 3 the frame head at a child's open and return
+                                         // node's open, 1 the sphere at a hit, 2 the object record at a light step
+                                         // (round 5 also probed the frame heads: DESIGN.md §4)
 #endif
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST

@@ -955,30 +955,75 @@ struct Cold {
 static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17>) == 192, "cold frame sizes");
 static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's frame is one 64-B half line");
 
+// One level's frame as the shading code sees it: the lane's Cold record and,
+// for deep shade trees (dense_heads(MAXF): depth > 4), the level's 32-B head
+// slot in a dense head array -- acc, f, meta and the first kHeadStack
+// medium-stack entries; the slots of one level for consecutive lanes are
+// consecutive, so a wave's heads share lines.  Stack entries from kHeadStack
+// on, and a refraction child's extension, stay in the Cold record.
+//
+// Why: a child's return reads its parent's head back after the child's
+// whole subtree, and with each head alone in a 128-B line of a 377-MB frame
+// area (C5) that read missed L2 nearly every time -- the head stream was
+// ~140 of C5's 266 GB read (the head-copy probe).  Dense heads:
+// C5 266 -> 166 GB read, +1.0 ... 1.4 %; C3 (depth 4) -0.2 ... -0.7 % with
+// them, so its instantiation keeps the plain frames (profiles/r05/ab/dense_heads_*).
+template <int MAXF, bool D = dense_heads(MAXF)>
+struct Fr {                          // plain frames (and MAXF = 1, which opens no child)
+    static constexpr bool kDense = false;
+    Cold<MAXF> *c;
+    __device__ __forceinline__ int stk(int i) const { return c->stack[i]; }
+    __device__ __forceinline__ void set_stk(int i, int v) const { c->stack[i] = v; }
+};
 template <int MAXF>
-__device__ __forceinline__ void cold_save_head(Cold<MAXF> &c, const HotR &h, float f) {
-    reinterpret_cast<f4v &>(c.head) = f4v{h.acc.r, h.acc.g, h.acc.b, f};
-    c.meta = h.meta;
+struct Fr<MAXF, true> {              // dense heads (dense_heads(MAXF))
+    static constexpr bool kDense = true;
+    Cold<MAXF> *c;
+    int *hs;
+    __device__ __forceinline__ int stk(int i) const { return i < kHeadStack ? hs[5 + i] : c->stack[i]; }
+    __device__ __forceinline__ void set_stk(int i, int v) const {
+        if (i < kHeadStack)
+            hs[5 + i] = v;
+        else
+            c->stack[i] = v;
+    }
+};
+template <int MAXF>
+__device__ __forceinline__ void cold_save_head(const Fr<MAXF> &fr, const HotR &h, float f) {
+    if constexpr (Fr<MAXF>::kDense) {
+        reinterpret_cast<f4v *>(fr.hs)[0] = f4v{h.acc.r, h.acc.g, h.acc.b, f};
+        fr.hs[4] = (int)h.meta;
+    } else {
+        Cold<MAXF> &c = *fr.c;
+        reinterpret_cast<f4v &>(c.head) = f4v{h.acc.r, h.acc.g, h.acc.b, f};
+        c.meta = h.meta;
+    }
 }
 template <int MAXF>
-__device__ __forceinline__ void cold_save_ext(Cold<MAXF> &c, V3 P, const HotR &h) {
-    f4v *v = reinterpret_cast<f4v *>(c.ext);
+__device__ __forceinline__ void cold_save_ext(const Fr<MAXF> &fr, V3 P, const HotR &h) {
+    f4v *v = reinterpret_cast<f4v *>(fr.c->ext);
     v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
     v[1] = f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei};
     v[2] = f4v{h.et, P.x, P.y, P.z};
 }
 // the head: h.acc, h.meta; returns f
 template <int MAXF>
-__device__ __forceinline__ float cold_restore_head(const Cold<MAXF> &c, HotR &h) {
-    const f4v a = reinterpret_cast<const f4v &>(c.head);
+__device__ __forceinline__ float cold_restore_head(const Fr<MAXF> &fr, HotR &h) {
+    f4v a;
+    if constexpr (Fr<MAXF>::kDense) {
+        a = reinterpret_cast<const f4v *>(fr.hs)[0];
+        h.meta = (unsigned)fr.hs[4];
+    } else {
+        a = reinterpret_cast<const f4v &>(fr.c->head);
+        h.meta = fr.c->meta;
+    }
     h.acc = {a.x, a.y, a.z};
-    h.meta = c.meta;
     return a.w;
 }
 // the rest of a refraction child's parent; returns its hit point
 template <int MAXF>
-__device__ __forceinline__ V3 cold_restore_ext(const Cold<MAXF> &c, HotR &h) {
-    const f4v *v = reinterpret_cast<const f4v *>(c.ext);
+__device__ __forceinline__ V3 cold_restore_ext(const Fr<MAXF> &fr, HotR &h) {
+    const f4v *v = reinterpret_cast<const f4v *>(fr.c->ext);
     const f4v a = v[0], b = v[1], d = v[2];
     h.N = {a.x, a.y, a.z};
     h.I = {a.w, b.x, b.y};
@@ -1090,9 +1135,9 @@ __device__ __forceinline__ float refl_fresnel(const ObjK &ob, float cosI) {
 }
 
 template <int MAXF>
-__device__ __forceinline__ bool in_stack(const Cold<MAXF> &f, int sn, int obj) {
+__device__ __forceinline__ bool in_stack(const Fr<MAXF> &f, int sn, int obj) {
     bool in = false;
-    for (int q = 0; q < sn; q++) in |= (f.stack[q] == obj);
+    for (int q = 0; q < sn; q++) in |= (f.stk(q) == obj);
     return in;
 }
 
@@ -1101,12 +1146,12 @@ __device__ __forceinline__ bool in_stack(const Cold<MAXF> &f, int sn, int obj) {
 // primary hit) is always {its own object} (main.cpp:751-757) and lives in no
 // frame.
 template <int MAXF>
-__device__ __forceinline__ void copy_stack(const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, bool root) {
+__device__ __forceinline__ void copy_stack(const HotR &f, const Fr<MAXF> &fc, const Fr<MAXF> &c, bool root) {
     if (root) {
-        c.stack[0] = f.obj;
+        c.set_stk(0, f.obj);
     } else {
         const int fsn = h_sn(f);
-        for (int q = 0; q < fsn; q++) c.stack[q] = fc.stack[q];
+        for (int q = 0; q < fsn; q++) c.set_stk(q, fc.stk(q));
     }
 }
 
@@ -1193,7 +1238,7 @@ __device__ __forceinline__ void ub_note(const Params &p, unsigned pix) {
 
 // Medium-stack transition for the refraction child (main.cpp:1021-1070).
 template <int MAXF, class CNT>
-__device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
+__device__ Medium refr_transition(const Params &p, const HotR &f, const Fr<MAXF> &fc, const Fr<MAXF> &c, int hit,
                                   bool root, CNT &cnt, unsigned pix) {
     const int fsn = h_sn(f);
     copy_stack(f, fc, c, root);
@@ -1204,38 +1249,38 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
         if (hit == f.obj) {
             m.state = EXITING;
             if (n > 0) {
-                m.ei = row(p.objs, c.stack[n - 1]).eta;
+                m.ei = row(p.objs, c.stk(n - 1)).eta;
                 n--;
             } else {
                 m.ei = p.eta_bkg;            // back() on an empty vector: UB in the reference
                 RT_COUNT(cnt.ub++);
                 ub_note(p, pix);
             }
-            m.et = n > 0 ? row(p.objs, c.stack[n - 1]).eta : p.eta_bkg;
+            m.et = n > 0 ? row(p.objs, c.stk(n - 1)).eta : p.eta_bkg;
             if (n > 0) n--;
         } else {
             m.state = ENTERING;
             m.ei = f.et;
             m.et = hit_eta;
-            c.stack[n++] = hit;
+            c.set_stk(n++, hit);
         }
     } else if (n > 0) {
         if (!(root ? hit == f.obj : in_stack(fc, fsn, hit))) {
             m.state = ENTERING;
             m.ei = f.et;
             m.et = hit_eta;
-            c.stack[n++] = hit;
+            c.set_stk(n++, hit);
         } else {
             m.state = EXITING;
             m.ei = f.et;
-            m.et = row(p.objs, c.stack[n - 1]).eta;
+            m.et = row(p.objs, c.stk(n - 1)).eta;
             n--;
         }
     } else {
         m.state = ENTERING;
         m.ei = p.eta_bkg;
         m.et = hit_eta;
-        c.stack[0] = hit;
+        c.set_stk(0, hit);
         n = 1;
     }
     m.sn = n;
@@ -1244,7 +1289,7 @@ __device__ Medium refr_transition(const Params &p, const HotR &f, const Cold<MAX
 
 // Medium-stack transition for the reflection child (main.cpp:1134-1182).
 template <int MAXF>
-__device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAXF> &fc, Cold<MAXF> &c, int hit,
+__device__ Medium refl_transition(const Params &p, const HotR &f, const Fr<MAXF> &fc, const Fr<MAXF> &c, int hit,
                                   bool root) {
     const int fsn = h_sn(f);
     copy_stack(f, fc, c, root);
@@ -1257,14 +1302,14 @@ __device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAX
         if (n > 0) {
             if (!(root ? hit == f.obj : in_stack(fc, fsn, hit))) {
                 m.et = hit_eta;
-                c.stack[n++] = f.obj;        // pushes the incidence object, as the reference does
+                c.set_stk(n++, f.obj);        // pushes the incidence object, as the reference does
             } else {
-                m.et = row(p.objs, c.stack[n - 1]).eta;
+                m.et = row(p.objs, c.stk(n - 1)).eta;
                 n--;
             }
         } else {
             m.et = hit_eta;
-            c.stack[0] = hit;
+            c.set_stk(0, hit);
             n = 1;
         }
     } else {
@@ -1275,7 +1320,7 @@ __device__ Medium refl_transition(const Params &p, const HotR &f, const Cold<MAX
         } else {
             m.state = ENTERING;
             m.et = hit_eta;
-            c.stack[n++] = hit;
+            c.set_stk(n++, hit);
         }
     }
     m.sn = n;
@@ -1297,12 +1342,24 @@ struct LaneState {
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         return reinterpret_cast<Cold<MAXF> *>(frames) + ((size_t)blockIdx.x * kBlock + t) * MAXF;
     }
-#if RT_PROBE & 8
-    void *frames2;
-    __device__ __forceinline__ Cold<MAXF> *cold2() const {
-        return reinterpret_cast<Cold<MAXF> *>(frames2) + ((size_t)blockIdx.x * kBlock + threadIdx.x) * MAXF;
+    // level k's frame; the dense heads (dense_heads) follow the frames and
+    // the spill area in the same buffer, 256-B aligned (rt_scene.cpp
+    // launch_one), [level][lane] 32-B slots -- addressed where used, like the
+    // frames, rather than held in registers across the traversal
+    __device__ __forceinline__ Fr<MAXF> fr(const Params &p, int k) const {
+        Fr<MAXF> f;
+        f.c = cold() + k;
+        if constexpr (Fr<MAXF>::kDense) {
+        unsigned t;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
+        const size_t lanes = (size_t)gridDim.x * kBlock;
+        const size_t off = (lanes * MAXF * sizeof(Cold<MAXF>) + lanes * (size_t)p.ovf_stride * sizeof(int) + 255) / 256 * 256;
+        // (slot index < 2^25: levels <= 17, lanes of the grid < 2^20)
+        f.hs = reinterpret_cast<int *>(static_cast<char *>(frames) + off) +
+               (size_t)(((unsigned)k * gridDim.x + blockIdx.x) * kBlock + t) * 8;
+        }
+        return f;
     }
-#endif
 };
 
 __device__ __forceinline__ void shadow_query(Query &q, const Params &p, int light, int self) {
@@ -1447,7 +1504,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
                 RT_COUNT(cnt.skip++);                // tmp_transparency stays 0
                 set_phase(h, PH_REFL);
             } else if (q.win >= 0) {
-                m = refr_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0, cnt, pix);
+                m = refr_transition(p, h, ls.fr(p, top > 0 ? top - 1 : 0), ls.fr(p, top), q.win, top == 0, cnt, pix);
                 set_phase(h, PH_REFR_CHILD);
                 open = true;
             } else {
@@ -1458,7 +1515,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             }
         } else {                                     // PH_REFL
             if (q.win >= 0) {
-                m = refl_transition(p, h, ls.cold()[top > 0 ? top - 1 : 0], ls.cold()[top], q.win, top == 0);
+                m = refl_transition(p, h, ls.fr(p, top > 0 ? top - 1 : 0), ls.fr(p, top), q.win, top == 0);
                 set_phase(h, PH_REFL_CHILD);
                 open = true;
             } else {
@@ -1469,13 +1526,10 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             }
         }
         if (open) {                                  // the recursion: save the parent
-            Cold<MAXF> &c = ls.cold()[top];
+            const Fr<MAXF> c = ls.fr(p, top);
             // dif.r: F_t (refraction child) or F_r (reflection child)
             if (h_phase(h) == PH_REFR_CHILD) cold_save_ext(c, q.o, h);
             cold_save_head(c, h, h.dif.r);
-#if RT_PROBE & 8
-            cold_save_head(ls.cold2()[top], h, h.dif.r);     // traffic probe: the head again, in a copy
-#endif
             top++;
         }
     }
@@ -1517,7 +1571,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
                 closest_query(q, p, T, h.obj);
                 const int sn = h_sn(h);
                 q.skipchk = (sn > 0) && !ob.is_sphere;
-                q.back = sn > 0 ? (top == 0 ? h.obj : ls.cold()[top - 1].stack[sn - 1]) : -1;
+                q.back = sn > 0 ? (top == 0 ? h.obj : ls.fr(p, top - 1).stk(sn - 1)) : -1;
                 set_phase(h, PH_REFR);
                 lds_store_phase(h);
                 ls.top = top;
@@ -1547,14 +1601,8 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             return RK_NONE;
         }
         top--;
-        const Cold<MAXF> &pc = ls.cold()[top];
+        const Fr<MAXF> pc = ls.fr(p, top);
         const float f = cold_restore_head(pc, h);
-#if RT_PROBE & 8
-        {   // traffic probe: the copy's head read back (never true)
-            HotR h2 = h;
-            if (cold_restore_head(ls.cold2()[top], h2) == -12345.0f && h2.meta == 0xdeadbeefu) h.acc.r = 0.0f;
-        }
-#endif
         if (h_phase(h) == PH_REFR_CHILD) {           // main.cpp:1072-1083
             q.o = cold_restore_ext(pc, h);
             h.dif.r = f;                             // F_t
@@ -1636,9 +1684,6 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     LaneState<MAXF> ls;
     ls.top = -1;
     ls.frames = p.frames;
-#if RT_PROBE & 8
-    ls.frames2 = p.frames2;
-#endif
     CountersT<COUNT> cnt = {0, 0, 0, 0, 0};
     unsigned long long w_prim = 0, w_shadow = 0, w_refr = 0, w_refl = 0;   // per wave (uniform)
     unsigned w_known = 0, w_bf = 0;
