@@ -141,6 +141,7 @@ struct Params {
     int lights_in_lds;                   // 1: the lights are staged in LDS; 0: read from `lights` (too many)
     const int *__restrict__ objleaf;     // BVH: per object, the link of its leaf in the main tree
     int org_first;                       // origin-leaf pass: bit 0 shadow, 1 refraction, 2 reflection rays
+    void *heads;                         // dense frame heads (dense_heads(MAXF)): [block][level][lane] 32-B slots
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -196,8 +197,8 @@ constexpr long long kFrameShare = RT_FRAME_SHARE;
 #endif
 constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 #ifndef RT_DENSE_HEADS_MIN
-#define RT_DENSE_HEADS_MIN 9             // instantiations with MAXF >= this keep their frame heads in a dense
-                                         // [level][lane] array (rt_kernels.hip Fr): depth > 4
+#define RT_DENSE_HEADS_MIN 2             // instantiations with MAXF >= this keep their frame heads in a dense
+                                         // [block][level][lane] array (rt_kernels.hip Fr): every recursive one
 #endif
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }

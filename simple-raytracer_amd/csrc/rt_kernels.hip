@@ -956,18 +956,20 @@ static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17
 static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's frame is one 64-B half line");
 
 // One level's frame as the shading code sees it: the lane's Cold record and,
-// for deep shade trees (dense_heads(MAXF): depth > 4), the level's 32-B head
+// in the recursive instantiations (dense_heads(MAXF)), the level's 32-B head
 // slot in a dense head array -- acc, f, meta and the first kHeadStack
-// medium-stack entries; the slots of one level for consecutive lanes are
-// consecutive, so a wave's heads share lines.  Stack entries from kHeadStack
+// medium-stack entries; the slots of one level for consecutive lanes of a
+// workgroup are consecutive, so a wave's heads share lines.  Stack entries from kHeadStack
 // on, and a refraction child's extension, stay in the Cold record.
 //
 // Why: a child's return reads its parent's head back after the child's
 // whole subtree, and with each head alone in a 128-B line of a 377-MB frame
 // area (C5) that read missed L2 nearly every time -- the head stream was
-// ~140 of C5's 266 GB read (the head-copy probe).  Dense heads:
-// C5 266 -> 166 GB read, +1.0 ... 1.4 %; C3 (depth 4) -0.2 ... -0.7 % with
-// them, so its instantiation keeps the plain frames (profiles/r05/ab/dense_heads_*).
+// ~140 of C5's 266 GB read (the head-copy probe).  Dense heads
+// ([block][level][lane], from Params::heads): C5 266 -> 166 GB read, +2.1 %;
+// C3 3.5 -> 2.0 GB read, +0.4 % (profiles/r05/ab/dense_heads_*).  (Addressed
+// [level][lane] over the whole grid instead, the slot arithmetic cost C3
+// 0.2 ... 0.7 %.)
 template <int MAXF, bool D = dense_heads(MAXF)>
 struct Fr {                          // plain frames (and MAXF = 1, which opens no child)
     static constexpr bool kDense = false;
@@ -1342,21 +1344,18 @@ struct LaneState {
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         return reinterpret_cast<Cold<MAXF> *>(frames) + ((size_t)blockIdx.x * kBlock + t) * MAXF;
     }
-    // level k's frame; the dense heads (dense_heads) follow the frames and
-    // the spill area in the same buffer, 256-B aligned (rt_scene.cpp
-    // launch_one), [level][lane] 32-B slots -- addressed where used, like the
-    // frames, rather than held in registers across the traversal
+    // level k's frame; the dense heads (dense_heads: Params::heads, after the
+    // frames and the spill area, rt_scene.cpp launch_one) are [block][level]
+    // [lane] 32-B slots -- addressed where used, like the frames, rather than
+    // held in registers across the traversal
     __device__ __forceinline__ Fr<MAXF> fr(const Params &p, int k) const {
         Fr<MAXF> f;
         f.c = cold() + k;
         if constexpr (Fr<MAXF>::kDense) {
         unsigned t;
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
-        const size_t lanes = (size_t)gridDim.x * kBlock;
-        const size_t off = (lanes * MAXF * sizeof(Cold<MAXF>) + lanes * (size_t)p.ovf_stride * sizeof(int) + 255) / 256 * 256;
         // (slot index < 2^25: levels <= 17, lanes of the grid < 2^20)
-        f.hs = reinterpret_cast<int *>(static_cast<char *>(frames) + off) +
-               (size_t)(((unsigned)k * gridDim.x + blockIdx.x) * kBlock + t) * 8;
+        f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * 8;
         }
         return f;
     }

@@ -249,10 +249,10 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     pl.work_shift = parts >= 8 ? 3 : parts >= 4 ? 2 : parts >= 2 ? 1 : 0;
     const size_t cold_bytes = (size_t)grid * kBlock * maxf * cold_frame_bytes(maxf);
     size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
-    // deep shade trees (dense_heads): the frame heads, [level][lane] 32-B
-    // slots, after the spill area (the kernel derives their address the same
-    // way: LaneState::fr)
-    if (dense_heads(maxf)) fbytes = (fbytes + 255) / 256 * 256 + (size_t)grid * kBlock * maxf * 32;
+    // recursive instantiations (dense_heads): the frame heads, [block][level]
+    // [lane] 32-B slots, after the spill area (Params::heads, LaneState::fr)
+    const size_t heads_off = (fbytes + 255) / 256 * 256;
+    if (dense_heads(maxf)) fbytes = heads_off + (size_t)grid * kBlock * maxf * 32;
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
@@ -268,6 +268,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     tm.mark("frames");
     pl.frames = slot.d_frames;
     pl.ovf = reinterpret_cast<int *>(static_cast<char *>(slot.d_frames) + cold_bytes);
+    pl.heads = dense_heads(maxf) ? static_cast<char *>(slot.d_frames) + heads_off : nullptr;
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
     s->last_lds = (long long)shm;
