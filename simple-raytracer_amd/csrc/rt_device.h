@@ -142,6 +142,9 @@ struct Params {
     const int *__restrict__ objleaf;     // BVH: per object, the link of its leaf in the main tree
     int org_first;                       // origin-leaf pass: bit 0 shadow, 1 refraction, 2 reflection rays
     void *heads;                         // dense frame heads (dense_heads(MAXF)): [block][level][lane] 32-B slots
+#if RT_DENSE_EXT
+    void *exts;                          // dense refraction extensions: [block][level][lane] 64-B slots (A/B)
+#endif
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -203,6 +206,9 @@ constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
 constexpr int kHeadStack = 3;            // medium-stack entries in a dense head slot
+#ifndef RT_DENSE_EXT
+#define RT_DENSE_EXT 0
+#endif
 #ifndef RT_PROBE
 #define RT_PROBE 0                       // traffic probes (measurement builds only): bit 0 the object record at a
                                          // node's open, 1 the sphere at a hit, 2 the object record at a light step

@@ -982,6 +982,9 @@ struct Fr<MAXF, true> {              // dense heads (dense_heads(MAXF))
     static constexpr bool kDense = true;
     Cold<MAXF> *c;
     int *hs;
+#if RT_DENSE_EXT
+    f4v *xs;                         // the level's dense extension slot (3 x 16 B)
+#endif
     __device__ __forceinline__ int stk(int i) const { return i < kHeadStack ? hs[5 + i] : c->stack[i]; }
     __device__ __forceinline__ void set_stk(int i, int v) const {
         if (i < kHeadStack)
@@ -1003,7 +1006,15 @@ __device__ __forceinline__ void cold_save_head(const Fr<MAXF> &fr, const HotR &h
 }
 template <int MAXF>
 __device__ __forceinline__ void cold_save_ext(const Fr<MAXF> &fr, V3 P, const HotR &h) {
+#if RT_DENSE_EXT
+    f4v *v;
+    if constexpr (Fr<MAXF>::kDense)
+        v = fr.xs;
+    else
+        v = reinterpret_cast<f4v *>(fr.c->ext);
+#else
     f4v *v = reinterpret_cast<f4v *>(fr.c->ext);
+#endif
     v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
     v[1] = f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei};
     v[2] = f4v{h.et, P.x, P.y, P.z};
@@ -1025,7 +1036,15 @@ __device__ __forceinline__ float cold_restore_head(const Fr<MAXF> &fr, HotR &h) 
 // the rest of a refraction child's parent; returns its hit point
 template <int MAXF>
 __device__ __forceinline__ V3 cold_restore_ext(const Fr<MAXF> &fr, HotR &h) {
+#if RT_DENSE_EXT
+    const f4v *v;
+    if constexpr (Fr<MAXF>::kDense)
+        v = fr.xs;
+    else
+        v = reinterpret_cast<const f4v *>(fr.c->ext);
+#else
     const f4v *v = reinterpret_cast<const f4v *>(fr.c->ext);
+#endif
     const f4v a = v[0], b = v[1], d = v[2];
     h.N = {a.x, a.y, a.z};
     h.I = {a.w, b.x, b.y};
@@ -1356,6 +1375,9 @@ struct LaneState {
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         // (slot index < 2^25: levels <= 17, lanes of the grid < 2^20)
         f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * 8;
+#if RT_DENSE_EXT
+        f.xs = static_cast<f4v *>(p.exts) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * 4;
+#endif
         }
         return f;
     }

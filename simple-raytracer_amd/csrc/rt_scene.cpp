@@ -253,6 +253,10 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     // [lane] 32-B slots, after the spill area (Params::heads, LaneState::fr)
     const size_t heads_off = (fbytes + 255) / 256 * 256;
     if (dense_heads(maxf)) fbytes = heads_off + (size_t)grid * kBlock * maxf * 32;
+#if RT_DENSE_EXT
+    const size_t exts_off = fbytes;
+    if (dense_heads(maxf)) fbytes += (size_t)grid * kBlock * maxf * 64;
+#endif
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
@@ -269,6 +273,9 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     pl.frames = slot.d_frames;
     pl.ovf = reinterpret_cast<int *>(static_cast<char *>(slot.d_frames) + cold_bytes);
     pl.heads = dense_heads(maxf) ? static_cast<char *>(slot.d_frames) + heads_off : nullptr;
+#if RT_DENSE_EXT
+    pl.exts = dense_heads(maxf) ? static_cast<char *>(slot.d_frames) + exts_off : nullptr;
+#endif
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
     s->last_lds = (long long)shm;
