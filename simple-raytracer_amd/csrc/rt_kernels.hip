@@ -576,8 +576,17 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     };
     // LDS holds stack entries [0, kLdsStack); entry 0 is kEmpty, or kRefill + b
     // when b blocks of kSpill older entries wait in device memory (ovf).
-    auto ovf_lane = [&]() -> int * {
-        return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * p.ovf_stride;
+#ifndef RT_DENSE_SPILL
+#define RT_DENSE_SPILL 1
+#endif
+    // spilled block b of this lane: [workgroup][block][lane] -- a wave's
+    // lanes' block b in adjacent bytes, like the dense frame heads (C5 +0.7 %,
+    // reads 166 -> 154 GB; profiles/r05/ab/dense_spill_*), or (RT_DENSE_SPILL
+    // 0) per lane contiguous
+    auto ovf_block = [&](int b) -> int * {
+        if (RT_DENSE_SPILL)
+            return p.ovf + (((size_t)blockIdx.x * (p.ovf_stride / kSpill) + b) * kBlock + threadIdx.x) * kSpill;
+        return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * p.ovf_stride + b * kSpill;
     };
     // RT_CHECK builds (lib_check/, not the benched library): the stack-bottom
     // invariant -- entry 0 is kEmpty, or kRefill + b with 1 <= b blocks in
@@ -597,7 +606,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         const int tag = stk[0];
         const int nb = tag == rtbvh::kEmpty ? 0 : tag - kRefill;
         if (!check(bottom_ok(tag) && (nb + 1) * kSpill <= p.ovf_stride && sp <= p.stack_cap)) return;
-        int *o = ovf_lane() + nb * kSpill;
+        int *o = ovf_block(nb);
         for (int i = 0; i < kSpill; i++) o[i] = stk[(1 + i) * kBlock];
         for (int i = kSpill + 1; i < sp; i++) stk[(i - kSpill) * kBlock] = stk[i * kBlock];
         sp -= kSpill;
@@ -612,7 +621,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         if ((unsigned)n - (unsigned)kRefill - 1u < (unsigned)(kStackMax / kSpill)) {   // rare: bring a block back
             const int nb = n - kRefill;
             if (!check(sp == 0 && n == stk[0] && bottom_ok(n))) return rtbvh::kEmpty;
-            const int *o = ovf_lane() + (nb - 1) * kSpill;
+            const int *o = ovf_block(nb - 1);
             for (int i = 0; i < kSpill; i++) stk[(1 + i) * kBlock] = o[i];
             stk[0] = nb > 1 ? n - 1 : rtbvh::kEmpty;
             sp = kSpill;
