@@ -455,15 +455,18 @@ def main() -> None:
                 # every core the process may run on (its affinity) -- and, when
                 # the lease's OMP_NUM_THREADS share is smaller, that share too:
                 # a lease whose cgroup gives it the time of only some of the CPUs
-                # it sees runs the oversubscribed affinity count slower
-                cpu_port = cpu_port_baseline(args.config, 8 * args.cpu_sample)
-                h = cpu_port["host"]
+                # it sees runs the oversubscribed affinity count slower.  The
+                # baseline is the faster of the two (the port on
+                # every core the host actually delivers)
+                runs = [cpu_port_baseline(args.config, 8 * args.cpu_sample)]
+                h = runs[0]["host"]
                 share = h["omp_num_threads"] or (int(h["cgroup_cpus"]) if h["cgroup_cpus"] else 0)
                 if 0 < share < h["affinity"]:
-                    cpu_port["at_lease_share"] = cpu_port_baseline(args.config, 8 * args.cpu_sample,
-                                                                   threads=share)
-                    cpu_port["note"] = ("value/cores: all affinity CPUs; at_lease_share: the lease's "
-                                        "OMP_NUM_THREADS share (faster when the cgroup quota is that share)")
+                    runs.append(cpu_port_baseline(args.config, 8 * args.cpu_sample, threads=share))
+                cpu_port = dict(max(runs, key=lambda r: r["value"]))
+                cpu_port["runs"] = [{k: r[k] for k in ("value", "cores", "sample")} for r in runs]
+                cpu_port["note"] = ("the faster of the port on every affinity CPU and on the lease's "
+                                    "OMP_NUM_THREADS / cgroup share (runs: both)")
             except Exception as e:
                 cpu_port = {"error": repr(e)}
         line = {
@@ -528,15 +531,20 @@ def main() -> None:
                                  "achieved_GBps": round(alg_bytes / k_s / 1e9, 3),
                                  "peak_GBps": PEAK_HBM_GBPS,
                                  "frac": round(alg_bytes / k_s / 1e9 / PEAK_HBM_GBPS, 7)}},
-            # (without oracle/_ref's reference binary: the port, kind "port")
-            "cpu_baseline": cpu if cpu is not None else cpu_port,
-            "cpu_port": cpu_port,
-            "verified": verified_rows,
-            "verified_note": "every rank's rows of the last timed frame (render_kernel without counters) equal "
-                             "bit for bit (NaN for NaN) the counting instantiation's render of the same rows, "
-                             "which the parity tests pin to the oracle"
-                             + ("; --verify: the gathered image equals one whole-image render" if verified
-                                else ""),
+            # the baseline is the C restatement on the host's
+            # cores (kind "port"); the real reference binary on one core is the
+            # anchor beside it (kind "reference")
+            "cpu_baseline": cpu_port if cpu_port is not None and "error" not in cpu_port else cpu,
+            "cpu_reference_anchor": cpu,
+            "verified": (None if verified_rows is None and verified is None
+                         else all(v for v in (verified_rows, verified) if v is not None)),
+            "verified_rows": verified_rows,
+            "verified_gather": verified,
+            "verified_note": "verified_rows: every rank's rows of the last timed frame (render_kernel without "
+                             "counters) equal bit for bit (NaN for NaN) the counting instantiation's render "
+                             "of the same rows, which the parity tests pin to the oracle; verified_gather "
+                             "(--verify, rank 0): the gathered image equals one whole-image render; "
+                             "verified: every check that ran passed",
             "ray_counts": {k: int(getattr(st, k)) for k in ("primary", "shadow", "refraction",
                                                              "reflection", "skip_trans", "ub_back")},
         }

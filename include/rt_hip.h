@@ -258,10 +258,6 @@ int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *
  * "bvh_presplit" (0..8, default 0: faces whose shadow factor is 0 or 1 enter
  * the BVH as up to that many references with clipped boxes -- never changes
  * the image; measured per scene, not a default),
- * "hot_copies" (0, or a power of 2 up to 64: copies of the main BVH's top
- * 64 nodes and their leaves, each wave starting its searches in one of them --
- * spreads the reads every search makes of the root over L2 channels; never
- * changes the image),
  * "counters" (1, the default: the kernel instantiation that counts rays and
  * executed tests for rt_stats; 0: the one without counters, which bench.py
  * times -- its stats report no rays; never changes the image),
@@ -282,14 +278,14 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * RT_PROF builds also [25] work counter drained, [27] sum of per-wave tails, [28] sum of wave
  * lifetimes, [29] waves; [32] known-zero shadow rays, [33] brute-force queries, [34] stack
  * spills (as in rt_stats), [35] BVH queries with a NaN origin or direction
- * (no hit; not searched); RT_PROF builds: [36..38] traversal trips of primary /
+ * (no hit; not searched; counting instantiation only); RT_PROF builds: [36..38] traversal trips of primary /
  * shadow / refraction + reflection queries, [39] trace steps whose wave searched
  * primary and other rays together; more launch facts: [40] origin-leaf pass
  * bits in effect (option org_first), [41] the scene's density (objects a line
  * across it meets, x1000), [42] BVH stack entries in LDS, [43] lights staged
- * in LDS (1) or read from device memory (0), [44] copies of the BVH's top in
- * effect (option hot_copies; on the device this slot counts the ub_back
- * events, which rt_scene_debug_ub_pixels returns), [45] work bands (option
+ * in LDS (1) or read from device memory (0), [44] 0 (on the device this slot
+ * counts the ub_back events, which rt_scene_debug_ub_pixels returns; rounds
+ * 4-5 reported the removed option hot_copies here), [45] work bands (option
  * work_parts), [48] the counting kernel instantiation (option counters: 1)
  * or the one without counters (0); RT_CHECK builds: [49] stack-bottom
  * invariant violations (must be 0).  n <= 64. */

@@ -590,67 +590,6 @@ void build_accel(const AccelInput &in, double D, const AccelOpts &o, AccelTree &
         for (auto &d : out.dirk)
             if (d.root >= 0) d.root *= (int)sizeof(rtbvh::NodeDev);
     }
-    // hot copies of the main tree's top (rt_accel.h, kHotNodes)
-    const int K = o.hot_copies;
-    if (ok && K > 1 && (K & (K - 1)) == 0 && !Q.nodes.empty()) {
-        const size_t nb = sizeof(rtbvh::NodeDev);
-        const int M = (int)std::min<size_t>(Q.nodes.size(), (size_t)kHotNodes);
-        auto up = [](size_t v, size_t a) { return (v + a - 1) / a * a; };
-        out.hot_copies = K;
-        out.hot_per_copy = M;
-        out.hot_base = up(QQ.size() * nb, 4096);
-        out.hot_stride = up((size_t)M * nb, 4096) + 256;   // another L2 channel for each copy
-        // the leaves the copied nodes link to, in first-seen order
-        std::vector<int32_t> leaves;
-        for (int i = 0; i < M; i++)
-            for (int32_t l : QQ[i].link)
-                if (l < 0 && l != rtbvh::kEmptyLeaf && std::find(leaves.begin(), leaves.end(), l) == leaves.end())
-                    leaves.push_back(l);
-        rec.resize(rec.size() - 3);                    // the padding goes after the copies
-        const size_t rec_main = rec.size();            // the main and cone trees' records end here
-        bool hot_ok = true;                            // a failed copy drops the copies, not the tree
-        for (int c = 0; c < K && hot_ok; c++) {
-            // this copy's records (16-word aligned + 16: another channel again)
-            rec.resize(up(rec.size(), 16) + (c ? 16 : 0), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-            std::vector<int32_t> remap(leaves.size());
-            for (size_t k = 0; k < leaves.size(); k++) {
-                int off, nfc, cnt;
-                rtbvh::leaf_decode(leaves[k], off, nfc, cnt);
-                const size_t words = 5 * (size_t)nfc + 2 * (size_t)(cnt - nfc);
-                const size_t noff = rec.size();
-                if (noff + words >= (size_t(1) << 23) - 1) {
-                    hot_ok = false;
-                    break;
-                }
-                rec.resize(noff + words);
-                std::copy(rec.begin() + off, rec.begin() + off + (long)words, rec.begin() + (long)noff);
-                remap[k] = -(1 + (int32_t)((noff << 8) | (size_t)(nfc << 4) | (size_t)cnt));
-            }
-            const size_t cbase = out.hot_base + (size_t)c * out.hot_stride;
-            for (int i = 0; i < M && hot_ok; i++) {
-                rtbvh::NodeDev z = QQ[i];
-                for (int32_t &l : z.link) {
-                    if (l >= 0) {
-                        const size_t child = (size_t)l / nb;    // main-array index
-                        if (child < (size_t)M) l = (int32_t)(cbase + child * nb);
-                    } else if (l != rtbvh::kEmptyLeaf) {
-                        l = remap[(size_t)(std::find(leaves.begin(), leaves.end(), l) - leaves.begin())];
-                    }
-                }
-                out.hot_nodes.push_back(z);
-            }
-        }
-        if (!hot_ok || out.hot_base + (size_t)K * out.hot_stride > (size_t)INT32_MAX) {
-            // the copies do not fit the link encoding: the main tree (valid
-            // before they were appended) renders without them, not the scan
-            rec.resize(rec_main);
-            out.hot_copies = 0;
-            out.hot_per_copy = 0;
-            out.hot_base = out.hot_stride = 0;
-            out.hot_nodes.clear();
-        }
-        rec.resize(rec.size() + 3, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    }
     out.ok = ok;
     out.dir_mode = dir_mode;
     out.depth = Q.depth;

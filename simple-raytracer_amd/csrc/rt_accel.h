@@ -65,18 +65,8 @@ struct AccelOpts {
     int collapse = 1;                  // binary -> 4-wide: 0 greedy, 1 SAH-optimal
     int node_milli = 500;              // SAH collapse: node visit cost, x1000 of a sphere test
     int threads = 0;                   // host threads for the build (0: automatic, 1: serial)
-    int hot_copies = 0;                // copies of the main tree's top nodes (0/1: none; else a power of 2)
     int presplit = 0;                  // references per face at most (0/1: one; build_accel's presplit)
 };
-
-// Copies of the top of the main tree (its first kHotNodes nodes in BFS order,
-// and the leaf records they link to): every trace starts at the root, so the
-// top nodes' few cache lines are read by every wave of an XCD through one L2
-// channel each; waves take copy k = wave mod hot_copies, each copy at another
-// offset (another channel).  The copies are identical but for their links:
-// a copied node links to its copy's nodes and records, or to the main tree's
-// nodes below the copied top.
-constexpr int kHotNodes = 64;
 
 // The device's trees, ready to upload.
 struct AccelTree {
@@ -93,12 +83,6 @@ struct AccelTree {
     int presplit = 0;                  // references per face at most, as built
     double sah = 0.0;                  // the main tree's SAH cost (node visits + primitive tests per ray, rt_accel.cpp)
     int threads = 1;                   // host threads used
-    // hot copies (AccelOpts::hot_copies): copy c's root at byte offset
-    // hot_base + c * hot_stride of the node buffer; hot_nodes holds the copies
-    // in order (hot_per_copy each); their records are appended to rec
-    int hot_copies = 0, hot_per_copy = 0;
-    size_t hot_base = 0, hot_stride = 0;
-    std::vector<rtbvh::NodeDev> hot_nodes;
     // host time per phase (ms): primitive boxes, binary SAH build, collapse +
     // BFS order, leaf records, quantisation, cone trees
     double ms[6] = {0, 0, 0, 0, 0, 0};

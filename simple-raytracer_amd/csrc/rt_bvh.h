@@ -336,21 +336,15 @@ inline void collapse_sah(const Result &R, ResultW<W> &Q, int max_leaf, float nod
 // 2 are (upper, lower) -- a ray reads the window that puts its near planes
 // first (word 2 when its direction along the axis is negative), so the device
 // selects near / far planes by a load offset, not by 4 v_cndmask per axis.
-#ifndef RT_NODE_PAD
-#define RT_NODE_PAD 0        // words of padding per node (6: 128-B nodes, one per L2 line)
-#endif
 struct Node4H {
     float origin[3];
     float scale;             // 2^e (-126 <= e <= kQExpMax), one for the three axes
     uint32_t ax[3][6];       // per axis: lo(0,1) lo(2,3) hi(0,1) hi(2,3) lo(0,1) lo(2,3)
     int32_t link[4];
-#if RT_NODE_PAD
-    uint32_t pad_[RT_NODE_PAD];
-#endif
     uint32_t lo(int a, int j) const { return ax[a][j]; }
     uint32_t hi(int a, int j) const { return ax[a][2 + j]; }
 };
-static_assert(sizeof(Node4H) == 104 + 4 * RT_NODE_PAD, "node4 device layout");
+static_assert(sizeof(Node4H) == 104, "node4 device layout");
 constexpr int kNodeAxisOff = 16;         // byte offset of axis 0's words; axis a at 16 + 24 a
 constexpr int kNodeLinkOff = 88;         // byte offset of the links
 
@@ -473,86 +467,6 @@ inline bool quantize_node(const Node4 &n, Node4H &z) {
     return true;
 }
 
-// 64-byte device node (round 5; RT_NODE8, after Ylitie et al. 2017 §3.2):
-// one node is one aligned half cache line, fetched by FOUR 16-B loads (the
-// 104-B Node4H takes five and straddles lines).  Per axis a: the node's box
-// origin o_a (the children's smallest lower bound, a float), a scale s_a (a
-// float >= extent / 255, rounded up so that o_a + 255 s_a covers the largest
-// upper bound) and each child's bounds as 8-bit multiples q of it -- lower
-// bounds rounded down, upper bounds up: child i's box on axis a is
-// [o_a + qlo s_a, o_a + qhi s_a] in real arithmetic, containing the float box.
-// Stored: words 0-2 the origin; 3-5 the scales times 2^24 (the device reads
-// a byte q as the binary16 subnormal q 2^-24 inside the plane FMA,
-// v_fma_mix_f32: the byte needs one mask or permute per two planes, no
-// conversion); 6-11 the byte planes lo_x hi_x lo_y hi_y lo_z hi_z (child i in
-// byte i); 12-15 the links.  The device selects near / far planes by the
-// ray's octant with one v_bfi per dword.
-struct Node4Q {
-    float origin[3];
-    float scale[3];          // s_a * 2^24
-    uint32_t pl[6];          // lo_x hi_x lo_y hi_y lo_z hi_z: child i's q in bits 8i..8i+7
-    int32_t link[4];
-};
-static_assert(sizeof(Node4Q) == 64, "node4q device layout");
-constexpr int kNodeQLinkOff = 48;        // byte offset of the links
-// Largest scale: the device forms s_a 2^24 * (1/d) with |1/d| capped at 2^64,
-// finite while s_a 2^24 < 2^63, i.e. s_a < 2^39 (node extents up to 255 * 2^38).
-constexpr double kQ8ScaleMax = 0x1p38;
-
-// One node of quantize8; false if a child box is not finite or the node is
-// too large for kQ8ScaleMax.
-inline bool quantize_node8(const Node4 &n, Node4Q &z) {
-    z = Node4Q{};
-    for (int i = 0; i < 4; i++) z.link[i] = n.link[i];
-    for (int a = 0; a < 3; a++) {
-        auto empty = [&](int i) { return n.link[i] == kEmpty || !(n.lo[a][i] <= n.hi[a][i]); };
-        double lo = INFINITY, hi = -INFINITY;
-        for (int i = 0; i < 4; i++) {
-            if (empty(i)) continue;
-            if (!std::isfinite(n.lo[a][i]) || !std::isfinite(n.hi[a][i])) return false;
-            lo = std::min(lo, (double)n.lo[a][i]);
-            hi = std::max(hi, (double)n.hi[a][i]);
-        }
-        if (!(lo <= hi)) lo = hi = 0.0;          // no child at all
-        const float o = (float)lo;               // exact: lo is a float
-        // s >= (hi - o) / 255, a normal float, with o + 255 s >= hi (double:
-        // exact for the operand ranges a tree holds); at least 2^-20 |o|, so
-        // that an empty slot's inverted box (o + 255 s > o) stays inverted
-        // after rounding (a padded primitive box spans far more)
-        float s = std::max({(float)((hi - (double)o) / 255.0), (float)std::ldexp(std::fabs((double)o), -20), 0x1p-100f});
-        while ((double)o + 255.0 * (double)s < hi) s = std::nextafter(s, INFINITY);
-        if (!((double)s <= kQ8ScaleMax)) return false;
-        z.origin[a] = o;
-        z.scale[a] = std::ldexp(s, 24);          // exact: a power-of-two scaling of a normal float
-        uint32_t L = 0, H = 0;
-        for (int i = 0; i < 4; i++) {
-            uint32_t ql = 255, qh = 0;           // empty slot: an inverted box (o + 255 s > o)
-            if (!empty(i)) {
-                double fl = std::floor(((double)n.lo[a][i] - (double)o) / (double)s);
-                fl = std::min(255.0, std::max(0.0, fl));
-                while (fl > 0 && (double)o + fl * (double)s > (double)n.lo[a][i]) fl -= 1;
-                double fh = std::ceil(((double)n.hi[a][i] - (double)o) / (double)s);
-                fh = std::min(255.0, std::max(0.0, fh));
-                while (fh < 255 && (double)o + fh * (double)s < (double)n.hi[a][i]) fh += 1;
-                ql = (uint32_t)fl;
-                qh = (uint32_t)fh;
-            }
-            L |= ql << (8 * i);
-            H |= qh << (8 * i);
-        }
-        z.pl[2 * a] = L;
-        z.pl[2 * a + 1] = H;
-    }
-    return true;
-}
-// child i's bounds on axis a as the device decodes them (real arithmetic)
-inline double node8_lo(const Node4Q &z, int a, int i) {
-    return (double)z.origin[a] + (double)((z.pl[2 * a] >> (8 * i)) & 255u) * std::ldexp((double)z.scale[a], -24);
-}
-inline double node8_hi(const Node4Q &z, int a, int i) {
-    return (double)z.origin[a] + (double)((z.pl[2 * a + 1] >> (8 * i)) & 255u) * std::ldexp((double)z.scale[a], -24);
-}
-
 // Returns false if a child box is not finite (NaN/inf geometry) or a node is
 // too large for kQExpMax: the caller then uses the brute-force scan.  Nodes
 // are independent: `threads` host threads share them.
@@ -565,34 +479,14 @@ inline bool quantize(const Result4 &Q, std::vector<Node4H> &out, int threads = 1
     });
     return ok.load();
 }
-inline bool quantize(const Result4 &Q, std::vector<Node4Q> &out, int threads = 1) {
-    out.assign(Q.nodes.size(), Node4Q{});
-    std::atomic<bool> ok{true};
-    parallel_ranges(Q.nodes.size(), threads, [&](size_t b, size_t e) {
-        for (size_t k = b; k < e; k++)
-            if (!quantize_node8(Q.nodes[k], out[k])) ok.store(false);
-    });
-    return ok.load();
-}
-
-// The device node format of this build: RT_NODE8 0 (default) -> Node4H
-// (104 B, binary16 planes with octant windows), 1 -> Node4Q (64 B, 8-bit
-// planes).  Round 5 measured the 64-B node against the 104-B one in one GPU
-// run, interleaved (profiles/r05/ab_node8_*.txt): C3 -4.1 %, C4 -6.3 %, C5
+// The device node format: Node4H (104 B, binary16 planes with octant
+// windows).  Round 5 measured a 64-B node with 8-bit planes against it in one
+// GPU run, interleaved (profiles/r05/ab_node8_*.txt): C3 -4.1 %, C4 -6.3 %, C5
 // -3.2 % -- one 16-B load fewer per node visit does not pay for the 18 VALU
-// instructions of its decode (6 octant selects, 12 byte shuffles) nor for the
-// 0.7-1 % more box tests of the coarser planes: the traversal is bound by its
-// VALU issue, not by the vector-memory path
-#ifndef RT_NODE8
-#define RT_NODE8 0
-#endif
-#if RT_NODE8
-using NodeDev = Node4Q;
-constexpr int kNodeDevLinkOff = kNodeQLinkOff;
-#else
+// instructions of its decode nor for the 0.7-1 % more box tests of the
+// coarser planes; removed in round 6 (git history keeps it).
 using NodeDev = Node4H;
 constexpr int kNodeDevLinkOff = kNodeLinkOff;
-#endif
 
 // Renumber Q's nodes breadth-first (root stays 0), so that the top levels of
 // the tree are nodes [0, K) for any K.

@@ -99,10 +99,6 @@ struct Params {
     const float4 *__restrict__ sscan;
     const float *__restrict__ ofac;      // (float)(1.0 - opacity) per object (main.cpp:909)
     const ObjK *__restrict__ objs;
-#if RT_PROBE
-    const ObjK *objs2;                   // (traffic probe builds: copies of objs / sscan read beside them)
-    const float4 *sscan2;
-#endif
     const FaceShadeK *__restrict__ fsh;
     const LightK *__restrict__ lights;
     const unsigned char *__restrict__ texels;   // all textures: RGB bytes, row-major
@@ -120,8 +116,6 @@ struct Params {
     // BVH (MODE_BVH): 8 float4 per 4-wide node (rt_bvh.h Node4), leaf-ordered object keys
     const float4 *__restrict__ bvh;
     int last_light_skip;                 // a last light with a Phong sum of 0 is not searched (advance)
-    int hot_base, hot_stride;            // copies of the main tree's top (rt_accel.h kHotNodes): the root
-    unsigned hot_mask;                   // wave w starts at bvh + hot_base + (w & hot_mask) * hot_stride bytes
     const float4 *__restrict__ leafrec;  // leaf-ordered primitive records (rt_bvh.h leaf_records)
     int dir_bf;                          // directional lights in a scene with spheres: 0 none,
                                          // 1 brute-force scan, 2 faces by the BVH + shadow-region trees
@@ -142,9 +136,6 @@ struct Params {
     const int *__restrict__ objleaf;     // BVH: per object, the link of its leaf in the main tree
     int org_first;                       // origin-leaf pass: bit 0 shadow, 1 refraction, 2 reflection rays
     void *heads;                         // dense frame heads (dense_heads(MAXF)): [block][level][lane] 32-B slots
-#if RT_DENSE_EXT
-    void *exts;                          // dense refraction extensions: [block][level][lane] 64-B slots (A/B)
-#endif
 };
 
 enum Mode { MODE_SCAN = 0, MODE_SCAN_LDS = 1, MODE_BVH = 2 };
@@ -206,14 +197,6 @@ constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
 constexpr int kHeadStack = 3;            // medium-stack entries in a dense head slot
-#ifndef RT_DENSE_EXT
-#define RT_DENSE_EXT 0
-#endif
-#ifndef RT_PROBE
-#define RT_PROBE 0                       // traffic probes (measurement builds only): bit 0 the object record at a
-                                         // node's open, 1 the sphere at a hit, 2 the object record at a light step
-                                         // (round 5 also probed the frame heads: DESIGN.md §4)
-#endif
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

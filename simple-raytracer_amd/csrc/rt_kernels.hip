@@ -275,8 +275,7 @@ __device__ __forceinline__ f4v bldv(__amdgpu_buffer_rsrc_t r, int off, int imm) 
 }
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int off, int imm) { return f4(bldv(r, off, imm)); }
 
-static_assert(sizeof(rtbvh::Node4H) == 104 + 4 * RT_NODE_PAD && rtbvh::kNodeAxisOff == 16 && rtbvh::kNodeLinkOff == 88, "node layout");
-static_assert(sizeof(rtbvh::Node4Q) == 64 && rtbvh::kNodeQLinkOff == 48, "node8 layout");
+static_assert(sizeof(rtbvh::Node4H) == 104 && rtbvh::kNodeAxisOff == 16 && rtbvh::kNodeLinkOff == 88, "node layout");
 // uniform float4 at a byte offset (4-byte aligned), via the scalar unit
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ float4 sld4b(const void *p, int off) {
@@ -445,46 +444,6 @@ __device__ __forceinline__ float4 near_first(float4 w, bool neg) {
     return neg ? make_float4(w.z, w.w, w.x, w.y) : w;
 }
 
-// The same six plane distances from a 64-B node (rt_bvh.h Node4Q, RT_NODE8):
-// w0 = (o_x, o_y, o_z, S_x), w1 = (S_y, S_z, lo_x, hi_x), w2 = (lo_y, hi_y,
-// lo_z, hi_z), S_a = s_a 2^24; child i's q in byte i of a plane dword.  A
-// byte q, moved into a binary16 half (bits 0-7 of either half, the rest 0),
-// is the subnormal q 2^-24, which v_fma_mix_f32 converts exactly inside the
-// plane FMA: t = fma(q 2^-24, S_a / d_a, (o_a - org_a) / d_a).  Per axis the
-// ray's octant picks the near / far dword (m_a: all ones for a negative
-// direction; one v_bfi each), then one mask (children 0, 2) and one permute
-// (children 1, 3) per dword put the bytes in place -- 12 VALU per node visit
-// more than the binary16 windows, for one 16-B load and 40 bytes less.
-__device__ __forceinline__ unsigned bsel(unsigned m, unsigned a, unsigned b) { return (m & a) | (~m & b); }
-__device__ __forceinline__ ChildPlanes child_planes8(float4 w0, float4 w1, float4 w2, float ix, float iy, float iz,
-                                                     float ox, float oy, float oz, unsigned mx, unsigned my,
-                                                     unsigned mz) {
-    const float A[3] = {ix * w0.w, iy * w1.x, iz * w1.y};
-    const float B[3] = {fmaf(w0.x, ix, -ox), fmaf(w0.y, iy, -oy), fmaf(w0.z, iz, -oz)};
-    const unsigned L[3] = {__float_as_uint(w1.z), __float_as_uint(w2.x), __float_as_uint(w2.z)};
-    const unsigned H[3] = {__float_as_uint(w1.w), __float_as_uint(w2.y), __float_as_uint(w2.w)};
-    const unsigned M[3] = {mx, my, mz};
-    ChildPlanes cp;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const unsigned nw = bsel(M[a], H[a], L[a]), fw = bsel(M[a], L[a], H[a]);
-        // children 0, 2 (bytes 0, 2) and 1, 3 (bytes 1, 3) as binary16 pairs
-        const h2v n02 = __builtin_bit_cast(h2v, nw & 0x00ff00ffu);
-        const h2v n13 = __builtin_bit_cast(h2v, __builtin_amdgcn_perm(0u, nw, 0x0c030c01u));
-        const h2v f02 = __builtin_bit_cast(h2v, fw & 0x00ff00ffu);
-        const h2v f13 = __builtin_bit_cast(h2v, __builtin_amdgcn_perm(0u, fw, 0x0c030c01u));
-        cp.tn[a][0] = fmaf((float)n02[0], A[a], B[a]);
-        cp.tn[a][1] = fmaf((float)n13[0], A[a], B[a]);
-        cp.tn[a][2] = fmaf((float)n02[1], A[a], B[a]);
-        cp.tn[a][3] = fmaf((float)n13[1], A[a], B[a]);
-        cp.tf[a][0] = fmaf((float)f02[0], A[a], B[a]);
-        cp.tf[a][1] = fmaf((float)f13[0], A[a], B[a]);
-        cp.tf[a][2] = fmaf((float)f02[1], A[a], B[a]);
-        cp.tf[a][3] = fmaf((float)f13[1], A[a], B[a]);
-    }
-    return cp;
-}
-
 // Sort key of a child: the bits of its entry distance, kMissKey for a miss or
 // an empty slot (unused slots link to the empty leaf, kEmptyLeaf: entering one
 // is harmless, so no link test; their inverted boxes miss anyway).  The entry
@@ -527,24 +486,18 @@ __device__ __forceinline__ unsigned child_entry(const ChildPlanes &cp, int i, fl
 template <bool point, unsigned LEAF_WAIT = kLeafWait, class CNT>
 __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool org_pass = false, int root = 0,
                           V3 po = V3{0.0f, 0.0f, 0.0f}, float cone_k = 0.0f, float cone_h = 0.0f) {
-    // |1/d| capped at 2^100 (Node4H) or 2^64 (Node4Q; 1/0 -> the cap): the
-    // quantised planes' scale * (1/d) then never overflows (the builder keeps
-    // e <= kQExpMax = 27, or s_a < kQ8ScaleMax = 2^38), and the cap is
-    // conservative: an axis with |d| below 1/cap moves the ray by less than
-    // D / cap along it, far inside the 2^-16 D primitive padding
-    constexpr float kCap = RT_NODE8 ? 0x1p64f : 0x1p100f;
+    // |1/d| capped at 2^100 (1/0 -> the cap): the quantised planes' scale *
+    // (1/d) then never overflows (the builder keeps e <= kQExpMax = 27), and
+    // the cap is conservative: an axis with |d| below 1/cap moves the ray by
+    // less than D / cap along it, far inside the 2^-16 D primitive padding
+    constexpr float kCap = 0x1p100f;
     const float ix = point ? 1.0f : clampr(safe_rcp(q.d.x), -kCap, kCap);
     const float iy = point ? 1.0f : clampr(safe_rcp(q.d.y), -kCap, kCap);
     const float iz = point ? 1.0f : clampr(safe_rcp(q.d.z), -kCap, kCap);
     const bool neg_x = ix < 0.0f, neg_y = iy < 0.0f, neg_z = iz < 0.0f;
-#if RT_NODE8
-    // per axis: all ones when the direction is negative (near planes = upper bounds)
-    const unsigned m_x = neg_x ? ~0u : 0u, m_y = neg_y ? ~0u : 0u, m_z = neg_z ? ~0u : 0u;
-#else
     // per axis: the byte offset of the window with the near planes first
     // (rt_bvh.h Node4H: lo lo hi hi lo lo -- word 2 on for a negative direction)
     const int wo_x = neg_x ? 8 : 0, wo_y = neg_y ? 8 : 0, wo_z = neg_z ? 8 : 0;
-#endif
     const float ox = point ? po.x : q.o.x * ix, oy = point ? po.y : q.o.y * iy, oz = point ? po.z : q.o.z * iz;
     const float tlo = point ? 0.0f : q.tmin - fabsf(q.tmin) * 0x1p-16f;
     // directional shadow ray in a scene with spheres: this pass tests the
@@ -557,7 +510,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     // rejects such a ray at its root: its cone tests are comparisons.)
     if (!point && (__builtin_isnan(q.o.x) | __builtin_isnan(q.o.y) | __builtin_isnan(q.o.z) |
                    __builtin_isnan(q.d.x) | __builtin_isnan(q.d.y) | __builtin_isnan(q.d.z))) {
-        atomicAdd(&p.stats[35], 1ull);
+        RT_COUNT(atomicAdd(&p.stats[35], 1ull));   // counting instantiation only
         return;
     }
     float best = q.tmax;                       // closest: running min (kFltMax at start)
@@ -576,17 +529,11 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     };
     // LDS holds stack entries [0, kLdsStack); entry 0 is kEmpty, or kRefill + b
     // when b blocks of kSpill older entries wait in device memory (ovf).
-#ifndef RT_DENSE_SPILL
-#define RT_DENSE_SPILL 1
-#endif
     // spilled block b of this lane: [workgroup][block][lane] -- a wave's
     // lanes' block b in adjacent bytes, like the dense frame heads (C5 +0.7 %,
-    // reads 166 -> 154 GB; profiles/r05/ab/dense_spill_*), or (RT_DENSE_SPILL
-    // 0) per lane contiguous
+    // reads 166 -> 154 GB against per-lane blocks; profiles/r05/ab/dense_spill_*)
     auto ovf_block = [&](int b) -> int * {
-        if (RT_DENSE_SPILL)
-            return p.ovf + (((size_t)blockIdx.x * (p.ovf_stride / kSpill) + b) * kBlock + threadIdx.x) * kSpill;
-        return p.ovf + ((size_t)blockIdx.x * kBlock + threadIdx.x) * p.ovf_stride + b * kSpill;
+        return p.ovf + (((size_t)blockIdx.x * (p.ovf_stride / kSpill) + b) * kBlock + threadIdx.x) * kSpill;
     };
     // RT_CHECK builds (lib_check/, not the benched library): the stack-bottom
     // invariant -- entry 0 is kEmpty, or kRefill + b with 1 <= b blocks in
@@ -633,11 +580,7 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     // One 4-wide node (rt_bvh.h Node4H, child_planes): slab-test the
     // children, push the far hits, continue with the nearest, park the first
     // leaf reached.
-#if RT_NODE8
-    auto visit_q = [&](float4 w0, float4 w1, float4 w2, float4 w4) {
-#else
     auto visit_q = [&](float4 w0, float4 wx, float4 wy, float4 wz, float4 w4) {
-#endif
 #if RT_PROF
         cnt.trips++;
 #endif
@@ -648,12 +591,8 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         const int top0 = stk[(sp - 1) * kBlock];
         float thi = thi_now();
         int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
-#if RT_NODE8
-        const ChildPlanes cp = child_planes8(w0, w1, w2, ix, iy, iz, ox, oy, oz, m_x, m_y, m_z);
-#else
         const float4 wa[3] = {wx, wy, wz};
         const ChildPlanes cp = child_planes(w0, wa, ix, iy, iz, ox, oy, oz);
-#endif
         unsigned k[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -734,19 +673,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
     if (point)
         node = root;
     else if (!ended) {
-        // this wave's copy of the top of the tree (Params::hot_mask; the
-        // index counts the waves of one XCD: blockIdx.x / 8)
-        const int hw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x >> 3) * (kBlock / 64) + threadIdx.x / 64));
-        const int r0 = p.hot_base + (int)((unsigned)hw & p.hot_mask) * p.hot_stride;
-#if RT_NODE8
-        visit_q(sld4b(p.bvh, r0), sld4b(p.bvh, r0 + 16), sld4b(p.bvh, r0 + 32),
-                sld4b(p.bvh, r0 + rtbvh::kNodeQLinkOff));
-#else
-        visit_q(sld4b(p.bvh, r0), near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff), neg_x),
-                near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff + 24), neg_y),
-                near_first(sld4b(p.bvh, r0 + rtbvh::kNodeAxisOff + 48), neg_z),
-                sld4b(p.bvh, r0 + rtbvh::kNodeLinkOff));
-#endif
+        visit_q(sld4b(p.bvh, 0), near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff), neg_x),
+                near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff + 24), neg_y),
+                near_first(sld4b(p.bvh, rtbvh::kNodeAxisOff + 48), neg_z), sld4b(p.bvh, rtbvh::kNodeLinkOff));
     }
     for (;;) {
         while (node >= 0) {
@@ -756,25 +685,15 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
             // node = the node's byte offset (rt_scene.cpp): five buffer loads
             // at immediate offsets from it; each axis window at the ray's
             // near-first offset (wo_*: 0 or 8 bytes, per lane)
-#if RT_NODE8
-            // node = its byte offset: the 64-B node as four aligned 16-B loads
-            const float4 w0 = bld4(bvh_rs, node, 0), w1 = bld4(bvh_rs, node, 16), w2 = bld4(bvh_rs, node, 32);
-            const float4 w4 = bld4(bvh_rs, node, rtbvh::kNodeQLinkOff);
-#else
             const float4 w0 = bld4(bvh_rs, node, 0), w4 = bld4(bvh_rs, node, rtbvh::kNodeLinkOff);
             const float4 wx = bld4(bvh_rs, node + wo_x, rtbvh::kNodeAxisOff);
             const float4 wy = bld4(bvh_rs, node + wo_y, rtbvh::kNodeAxisOff + 24);
             const float4 wz = bld4(bvh_rs, node + wo_z, rtbvh::kNodeAxisOff + 48);
-#endif
 #if RT_PROF >= 2
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w4.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
 #endif
-#if RT_NODE8
-            visit_q(w0, w1, w2, w4);
-#else
             visit_q(w0, wx, wy, wz, w4);
-#endif
 #if RT_PROF >= 2
             cnt.t_trip += __builtin_amdgcn_s_memtime() - t_a;
 #endif
@@ -991,9 +910,6 @@ struct Fr<MAXF, true> {              // dense heads (dense_heads(MAXF))
     static constexpr bool kDense = true;
     Cold<MAXF> *c;
     int *hs;
-#if RT_DENSE_EXT
-    f4v *xs;                         // the level's dense extension slot (3 x 16 B)
-#endif
     __device__ __forceinline__ int stk(int i) const { return i < kHeadStack ? hs[5 + i] : c->stack[i]; }
     __device__ __forceinline__ void set_stk(int i, int v) const {
         if (i < kHeadStack)
@@ -1015,15 +931,7 @@ __device__ __forceinline__ void cold_save_head(const Fr<MAXF> &fr, const HotR &h
 }
 template <int MAXF>
 __device__ __forceinline__ void cold_save_ext(const Fr<MAXF> &fr, V3 P, const HotR &h) {
-#if RT_DENSE_EXT
-    f4v *v;
-    if constexpr (Fr<MAXF>::kDense)
-        v = fr.xs;
-    else
-        v = reinterpret_cast<f4v *>(fr.c->ext);
-#else
     f4v *v = reinterpret_cast<f4v *>(fr.c->ext);
-#endif
     v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
     v[1] = f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei};
     v[2] = f4v{h.et, P.x, P.y, P.z};
@@ -1045,15 +953,7 @@ __device__ __forceinline__ float cold_restore_head(const Fr<MAXF> &fr, HotR &h) 
 // the rest of a refraction child's parent; returns its hit point
 template <int MAXF>
 __device__ __forceinline__ V3 cold_restore_ext(const Fr<MAXF> &fr, HotR &h) {
-#if RT_DENSE_EXT
-    const f4v *v;
-    if constexpr (Fr<MAXF>::kDense)
-        v = fr.xs;
-    else
-        v = reinterpret_cast<const f4v *>(fr.c->ext);
-#else
     const f4v *v = reinterpret_cast<const f4v *>(fr.c->ext);
-#endif
     const f4v a = v[0], b = v[1], d = v[2];
     h.N = {a.x, a.y, a.z};
     h.I = {a.w, b.x, b.y};
@@ -1097,9 +997,6 @@ __device__ __forceinline__ HitRec hit_geometry(const Params &p, int obj, V3 o, V
     } else {
         float4 s = row(p.sscan, obj - p.nf);
         h.N = vnorm(vdiv(vsub(h.P, V3{s.x, s.y, s.z}), s.w));
-#if RT_PROBE & 2
-        if (row(p.sscan2, obj - p.nf).w == -12345.0f) h.N.x = 0.0f;   // traffic probe (never true)
-#endif
     }
     return h;
 }
@@ -1196,12 +1093,6 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
     const HitRec hr = hit_geometry(p, obj, o, d, t);
     V3 N = hr.N;
     const ObjK &ob = row(p.objs, obj);
-#if RT_PROBE & 1
-    {   // traffic probe: the same record's two sectors from a copy (never true)
-        const ObjK &o2 = row(p.objs2, obj);
-        if (o2.tex == -12345 && o2.dif[0] == -12345.0f) N.x = 0.0f;
-    }
-#endif
     V3 I = vmul(d, -1.0f);
     float cosI = vdot(N, I);
     C3 dif = {ob.dif[0], ob.dif[1], ob.dif[2]};
@@ -1384,9 +1275,6 @@ struct LaneState {
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         // (slot index < 2^25: levels <= 17, lanes of the grid < 2^20)
         f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * 8;
-#if RT_DENSE_EXT
-        f.xs = static_cast<f4v *>(p.exts) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * 4;
-#endif
         }
         return f;
     }
@@ -1470,12 +1358,6 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
             const int light = h_light(h);
             const ObjK &ob = row(p.objs, h.obj);
-#if RT_PROBE & 4
-            {   // traffic probe: the light step's fields from a copy (never true)
-                const ObjK &o2 = row(p.objs2, h.obj);
-                if (o2.spc[0] == -12345.0f && o2.n == -12345.0f) h.acc.r = 0.0f;
-            }
-#endif
             // the light's words in one batch (LightK: xyz w | col | L)
             const LightW lw = light_words(p, light);
             const f4v lw0 = lw.w0, lw1 = lw.w1, lw2 = lw.w2;
@@ -1661,11 +1543,7 @@ __device__ __forceinline__ int image_row(const Params &p, int r) {
 // bijection, so the image does not change.
 constexpr int kStrip = 8;   // 4 / 16-row strips: C3 -1.6 / -4 %, C5 -3.7 / -3.9 %
 __device__ __forceinline__ void pixel_xy(const Params &p, unsigned idx, int &x, int &y) {
-#ifdef RT_AB_NOPIX
-    if (false) {
-#else
-    if (p.pix) {
-#endif                 // a pixel list (rt_render_pixels): image coordinates
+    if (p.pix) {       // a pixel list (rt_render_pixels): image coordinates
         x = p.pix[2 * idx];
         y = p.pix[2 * idx + 1];
         return;
@@ -1778,15 +1656,8 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 // (x, y) from the work item again: two registers fewer live
                 // across the whole pixel; a pixel list's k-th colour goes to out[3k..]
                 int px = (int)pix_idx, py = 0;
-#ifndef RT_AB_NOPIX
-                if (!p.pix)
-#endif
-                    pixel_xy(p, pix_idx, px, py);
-#ifndef RT_AB_NOSTORE                // (A/B probe only: no framebuffer store)
+                if (!p.pix) pixel_xy(p, pix_idx, px, py);
                 *reinterpret_cast<f3v *>(p.out + ((size_t)py * p.W + px) * 3) = f3v{color.r, color.g, color.b};
-#else
-                if (color.r == -1.0f) p.out[0] = (float)px + (float)py;
-#endif
                 busy = false;
             }
         }
@@ -2084,14 +1955,16 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
 // bytes allow, else the row's own element type).
 template <typename T>
 __global__ void deinterleave_kernel(const T *__restrict__ gathered, int world, int rows_per, size_t n, int block,
-                                    T *__restrict__ image) {
-    const int y = blockIdx.y;
-    const int rank = (y / block) % world;
-    const int k = (y / (block * world)) * block + y % block;
-    const T *src = gathered + ((size_t)rank * rows_per + k) * n;
-    T *dst = image + (size_t)y * n;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        dst[i] = src[i];
+                                    int H, T *__restrict__ image) {
+    // rows grid-strided in y: the grid's y extent is capped at 65535
+    for (int y = blockIdx.y; y < H; y += gridDim.y) {
+        const int rank = (y / block) % world;
+        const int k = (y / (block * world)) * block + y % block;
+        const T *src = gathered + ((size_t)rank * rows_per + k) * n;
+        T *dst = image + (size_t)y * n;
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+            dst[i] = src[i];
+    }
 }
 
 // The P3 writer's values (main.cpp:760: (size_t)(int)(c * 255), rth_quantize)
@@ -2201,17 +2074,17 @@ hipError_t deinterleave_launch(const void *gathered, size_t row_bytes, size_t el
                      reinterpret_cast<uintptr_t>(image) % 16 == 0;
     const size_t eb = vec ? 16 : elem_bytes, n = row_bytes / eb;
     const unsigned gx = (unsigned)std::min<size_t>(64, (n + 255) / 256);
-    const dim3 grid(gx, (unsigned)H);
+    const dim3 grid(gx, (unsigned)std::min(H, 65535));
     if (vec)
         hipLaunchKernelGGL(deinterleave_kernel<uint4>, grid, dim3(256), 0, st, static_cast<const uint4 *>(gathered),
-                           world, rows_per, n, block, static_cast<uint4 *>(image));
+                           world, rows_per, n, block, H, static_cast<uint4 *>(image));
     else if (eb == 4)
         hipLaunchKernelGGL(deinterleave_kernel<unsigned>, grid, dim3(256), 0, st,
-                           static_cast<const unsigned *>(gathered), world, rows_per, n, block,
+                           static_cast<const unsigned *>(gathered), world, rows_per, n, block, H,
                            static_cast<unsigned *>(image));
     else
         hipLaunchKernelGGL(deinterleave_kernel<unsigned char>, grid, dim3(256), 0, st,
-                           static_cast<const unsigned char *>(gathered), world, rows_per, n, block,
+                           static_cast<const unsigned char *>(gathered), world, rows_per, n, block, H,
                            static_cast<unsigned char *>(image));
     return hipGetLastError();
 }

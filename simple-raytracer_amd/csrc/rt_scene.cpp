@@ -77,7 +77,6 @@ struct rt_scene {
     long long opt_fail_bvh_upload = 0; // test hook: the next BVH uploads fail (RT_E_NOMEM)
     AccelInput in;                     // host arrays + BVH sources (rt_accel.h)
     long long opt_bvh_threads = 0;     // host threads of the BVH build (0: automatic, 1: serial)
-    long long opt_hot_copies = 0;      // copies of the main tree's top (rt_accel.h kHotNodes; 0/1: none)
     long long opt_counters = kCounters;  // 1: the counting kernel (rt_stats' rays, events, tests); 0: none
     long long opt_frame_share = -1;    // the occupancy-sized grid / this: frames in flight that run side by
                                        // side (-1 auto: kFrameShare for small frames with inflight > 1, else 1)
@@ -98,7 +97,6 @@ struct rt_scene {
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
     long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0, last_work_parts = 0;
-    long long last_hot_copies = 0;
     long long bvh_nodes = 0;
     bool last_valid = false;
 };
@@ -123,6 +121,12 @@ hipStream_t take_stream(int device) {
             return st;
         }
     return nullptr;
+}
+bool pool_has(int device) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const auto &e : g_stream_pool)
+        if (e.first == device) return true;
+    return false;
 }
 void give_stream(int device, hipStream_t st) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -253,10 +257,6 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     // [lane] 32-B slots, after the spill area (Params::heads, LaneState::fr)
     const size_t heads_off = (fbytes + 255) / 256 * 256;
     if (dense_heads(maxf)) fbytes = heads_off + (size_t)grid * kBlock * maxf * 32;
-#if RT_DENSE_EXT
-    const size_t exts_off = fbytes;
-    if (dense_heads(maxf)) fbytes += (size_t)grid * kBlock * maxf * 64;
-#endif
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
@@ -273,9 +273,6 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     pl.frames = slot.d_frames;
     pl.ovf = reinterpret_cast<int *>(static_cast<char *>(slot.d_frames) + cold_bytes);
     pl.heads = dense_heads(maxf) ? static_cast<char *>(slot.d_frames) + heads_off : nullptr;
-#if RT_DENSE_EXT
-    pl.exts = dense_heads(maxf) ? static_cast<char *>(slot.d_frames) + exts_off : nullptr;
-#endif
     s->last_blocks_per_cu = nb;
     s->last_grid = grid;
     s->last_lds = (long long)shm;
@@ -299,7 +296,6 @@ int build_bvh(rt_scene *s, double D) {
     o.collapse = (int)s->opt_bvh_collapse;
     o.node_milli = (int)s->opt_bvh_node;
     o.threads = (int)s->opt_bvh_threads;
-    o.hot_copies = (int)s->opt_hot_copies;
     o.presplit = (int)s->opt_bvh_presplit;
     AccelTree T;
     StepTimer tm("build_bvh");
@@ -322,25 +318,18 @@ int build_bvh(rt_scene *s, double D) {
         ok = false;
     }
     if (ok) {
-        const size_t main_bytes = QQ.size() * sizeof(QQ[0]);
-        const size_t node_bytes = T.hot_copies > 1 ? T.hot_base + (size_t)T.hot_copies * T.hot_stride : main_bytes;
+        const size_t node_bytes = QQ.size() * sizeof(QQ[0]);
         const size_t dir_bytes = std::max<size_t>(1, dirk.size()) * sizeof(DirK);
         if (hipMalloc(&nb, node_bytes) != hipSuccess ||
             hipMalloc(&nr, std::max<size_t>(1, rec.size()) * sizeof(float4)) != hipSuccess ||
             hipMalloc(&nd, dir_bytes) != hipSuccess || hipMalloc(&nl, objleaf.size() * sizeof(int32_t)) != hipSuccess)
             rc = RT_E_NOMEM;
-        else if (hipMemcpy(nb, QQ.data(), main_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        else if (hipMemcpy(nb, QQ.data(), node_bytes, hipMemcpyHostToDevice) != hipSuccess ||
                  hipMemcpy(nr, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess ||
                  (!dirk.empty() && hipMemcpy(nd, dirk.data(), dirk.size() * sizeof(DirK), hipMemcpyHostToDevice) !=
                                        hipSuccess) ||
                  hipMemcpy(nl, objleaf.data(), objleaf.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
             rc = RT_E_HIP;
-        for (int c = 0; !rc && c < (T.hot_copies > 1 ? T.hot_copies : 0); c++) {
-            const size_t per = (size_t)T.hot_per_copy * sizeof(QQ[0]);
-            if (hipMemcpy(reinterpret_cast<char *>(nb) + T.hot_base + (size_t)c * T.hot_stride,
-                          T.hot_nodes.data() + (size_t)c * T.hot_per_copy, per, hipMemcpyHostToDevice) != hipSuccess)
-                rc = RT_E_HIP;
-        }
         if (rc) {
             if (nb) (void)hipFree(nb);
             if (nr) (void)hipFree(nr);
@@ -368,11 +357,6 @@ int build_bvh(rt_scene *s, double D) {
     s->base.leafrec = nr;
     s->base.dirk = nd;
     s->base.dir_bf = T.dir_mode;
-    const bool hot = ok && rc == RT_OK && T.hot_copies > 1;
-    s->base.hot_base = hot ? (int)T.hot_base : 0;
-    s->base.hot_stride = hot ? (int)T.hot_stride : 0;
-    s->base.hot_mask = hot ? (unsigned)(T.hot_copies - 1) : 0u;
-    s->last_hot_copies = hot ? T.hot_copies : 0;
     tm.mark("upload");
     s->bvh_ok = ok && rc == RT_OK;
     s->bvh_D = rc == RT_OK ? D : -1.0;   // a failed upload is retried; an unusable tree (scan) is not
@@ -581,9 +565,6 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
         const size_t o_fscan = a.add(in.fscan), o_sscan = a.add(in.sscan), o_ofac = a.add(in.ofac);
         const size_t o_objs = a.add(in.objs), o_fsh = a.add(in.fsh), o_lights = a.add(in.lights);
         const size_t o_texels = a.reserve(tex_bytes), o_texs = a.add(texs);
-#if RT_PROBE
-        const size_t o_objs2 = a.add(in.objs), o_sscan2 = a.add(in.sscan);
-#endif
         for (int i = 0; i < desc->n_textures; i++) {
             const rt_texture_desc &T = desc->textures[i];
             std::memcpy(a.host.data() + o_texels + (size_t)texs[i].off, T.rgb, (size_t)T.width * T.height * 3);
@@ -602,10 +583,6 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
             p.lights = reinterpret_cast<const LightK *>(d + o_lights);
             p.texels = reinterpret_cast<const unsigned char *>(d + o_texels);
             p.texs = reinterpret_cast<const TexK *>(d + o_texs);
-#if RT_PROBE
-            p.objs2 = reinterpret_cast<const ObjK *>(d + o_objs2);
-            p.sscan2 = reinterpret_cast<const float4 *>(d + o_sscan2);
-#endif
         }
     }
     tm.mark("uploads");
@@ -650,8 +627,6 @@ int rt_scene_create(int device, const rt_scene_desc *desc, rt_scene **out) {
     p.chunk = 0;                       // launch_one: chunk_for, refill_for
     p.refill_min = 1;
     p.gate_x = kGateX;
-    p.hot_base = p.hot_stride = 0;     // set with the BVH (build_bvh)
-    p.hot_mask = 0;
     // The origin-leaf pass for reflection and refraction rays pays in dense
     // scenes (C5: +2.3 %) and costs sparse ones (C3: -1.1 %;
     // profiles/r03/ab_origin_leaf.txt); the density is AccelInput::crossings
@@ -706,8 +681,10 @@ int rt_device_init(int device) {
             rc = RT_E_HIP;
     (void)hipFree(d);
     tm.mark("memory + copies");
+    // one waiting stream per device at most: a repeated call (the API allows
+    // it) adds no queue the process does not need (4 hardware queues each)
     hipStream_t st = nullptr;
-    if (!rc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+    if (!rc && !pool_has(device) && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
         if (hipStreamSynchronize(st) == hipSuccess) give_stream(device, st);
         else (void)hipStreamDestroy(st);
     }
@@ -779,11 +756,6 @@ int rt_scene_set_option(rt_scene *s, const char *key, long long value) {
         if (value < 0 || value > 1) return RT_E_INVALID;
         s->opt_recursive = value;
     }
-    else if (k == "hot_copies") {
-        if (value < 0 || value > 64 || (value & (value - 1))) return RT_E_INVALID;
-        s->opt_hot_copies = value;
-        s->bvh_D = -1.0;
-    }
     else return RT_E_INVALID;
     return RT_OK;
 }
@@ -851,7 +823,6 @@ int rt_render_pixels(rt_scene *s, const rt_camera *cam, int W, int H, const int 
 static int deinterleave(const void *gathered, size_t elem_bytes, int world, int rows_per, int W, int H, int block,
                         void *image, void *hip_stream) {
     if (!gathered || !image || world < 1 || rows_per < 1 || W < 1 || H < 1 || block < 1) return RT_E_INVALID;
-    if (H > 65535) return RT_E_UNSUPPORTED;
     // every image row's source row must exist: each rank's row count <= rows_per
     const int nblocks = (H + block - 1) / block;
     for (int r = 0; r < world; r++) {
@@ -980,7 +951,7 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[42] = (unsigned long long)s->last_stack_cap;
     h[43] = (unsigned long long)s->last_lights_in_lds;
     h[45] = (unsigned long long)s->last_work_parts;
-    h[44] = (unsigned long long)s->last_hot_copies;
+    h[44] = 0;                                   // (round 4-5: the BVH top copies, option removed)
     h[48] = (unsigned long long)s->opt_counters;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;

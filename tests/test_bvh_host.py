@@ -46,14 +46,12 @@ def test_bvh_device_padding_stack(checker):
 
 
 # Tree hashes (tools/bvh_bench.cpp: FNV-1a over the uploaded node, record,
-# object-leaf and cone-tree arrays) of the seeded benchmark scenes, by device
-# node size.  104: the round-3 builder's trees with binary16 nodes (RT_NODE8=0);
-# the round-4 builder (primitive array reordered in place, one-pass range
-# statistics, sparse bins for small ranges, subtrees on threads, bitwise
-# binary16 rounding) builds the same trees.  64: the same trees stored as the
-# round-5 64-B nodes with 8-bit planes (build option RT_NODE8=1).
-BENCH_TREE_HASH = {104: {"C3": "d0d4c36f4057bc62", "C4": "5023c92e900cccd1", "C5": "0fa041b2ecb60269"},
-                   64: {"C3": "04afc4732a2a9f6b", "C4": "a76af2eedeb8ab63", "C5": "c6ebbeb0f0baad7c"}}
+# object-leaf and cone-tree arrays) of the seeded benchmark scenes with the
+# 104-B binary16 device nodes: the round-3 builder's trees; the round-4
+# builder (primitive array reordered in place, one-pass range statistics,
+# sparse bins for small ranges, subtrees on threads, bitwise binary16
+# rounding) builds the same trees.
+BENCH_TREE_HASH = {104: {"C3": "d0d4c36f4057bc62", "C4": "5023c92e900cccd1", "C5": "0fa041b2ecb60269"}}
 
 
 @pytest.fixture(scope="module")
@@ -66,8 +64,7 @@ def bvh_bench():
 @pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
 def test_bvh_build_threads_identical(bvh_bench, tmp_path, cfg):
     """The host build on 4 threads gives the serial build's trees bit for bit,
-    and both are the pinned trees of the seeded scene (no GPU); a build with
-    hot copies of the tree's top holds the same tree from every copy's root."""
+    and both are the pinned trees of the seeded scene (no GPU)."""
     import json
     from rtamd import scenes as gen
     path = gen.write_scene(str(tmp_path), cfg)
@@ -76,6 +73,3 @@ def test_bvh_build_threads_identical(bvh_bench, tmp_path, cfg):
     j = json.loads(r.stdout)
     assert j["identical"] and j["ok"] == 1, j
     assert j["hash"] == BENCH_TREE_HASH[j["node_bytes"]][cfg], j
-    # 16 hot copies of the top (option hot_copies): each copy's walk reads
-    # the main tree's bounds and leaf records, the main arrays unchanged
-    assert j["hot_ok"] and j["hot_copies"] == 16 and j["hot_per_copy"] == min(64, j["main_nodes"]), j

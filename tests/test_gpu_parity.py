@@ -941,19 +941,15 @@ def test_last_light_skip_and_recursive_instantiation_bit_identical():
         rtamd.render_scene("test7_s.txt", cwd=SCENES, options={"recursive": 2})
 
 
-def test_work_bands_hot_copies_counters_bit_identical():
+def test_work_bands_counters_bit_identical():
     """Option work_parts (bands of the work items with a pixel counter each,
-    auto = one per XCD), option hot_copies (copies of the BVH's top 64
-    nodes and their leaves; each wave starts its searches in one) and option
-    counters (0: the kernel instantiation without the counters, which the
-    bench times) change which lane renders which pixel and where a search
-    reads the tree's top, never a pixel: the image and ray counts equal the default render's bit
-    for bit, which equals the oracle's.  C2 has fewer nodes than one copy
-    holds (the whole tree is copied), C5 at depth 8 has 37 864."""
-    variants = [{"work_parts": w} for w in (1, 2, 4, 8)]
-    variants += [{"hot_copies": k} for k in (0, 2, 16, 64)] + [{"hot_copies": 16, "work_parts": 1, "chunk": 100}]
+    auto = one per XCD) and option counters (0: the kernel instantiation
+    without the counters, which the bench times) change which lane renders
+    which pixel, never a pixel: the image and ray counts equal the default
+    render's bit for bit, which equals the oracle's."""
+    variants = [{"work_parts": w} for w in (1, 2, 4, 8)] + [{"work_parts": 1, "chunk": 100}]
     # the instantiation without counters renders the same image (its counts are 0)
-    variants += [{"counters": 0}, {"counters": 0, "work_parts": 1}, {"counters": 0, "hot_copies": 16}]
+    variants += [{"counters": 0}, {"counters": 0, "work_parts": 1}, {"counters": 0, "work_parts": 2, "chunk": 64}]
     for name, depth in (("C2_128x128.txt", None), ("C3_64x64.txt", None), ("C5_8x8.txt", 8)):
         ref, st = rtamd.render_scene(name, cwd=SCENES, depth=depth)
         o = OracleScene(name, cwd=SCENES)
@@ -971,17 +967,17 @@ def test_work_bands_hot_copies_counters_bit_identical():
                 assert st2.rays() == 0 and st2.box_tests == 0 and st2.kernel_ms > 0, (name, opts)
     hs = rtamd.HostScene("C3_64x64.txt", cwd=SCENES)
     gs = rtamd.GpuScene(hs)
-    gs.set_option("hot_copies", 16)
     gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
     dbg = gs.debug_counters()
-    assert dbg[44] == 16 and dbg[48] == 1 and dbg[45] == 8          # counted by default
+    assert dbg[44] == 0 and dbg[48] == 1 and dbg[45] == 8           # counted by default
     st1 = gs.last_stats()
     assert st1.box_tests > 0 and st1.sphere_tests > 0 and st1.face_tests > 0 and st1.rays() > 0
     gs.set_option("counters", 0)
     gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
     st0 = gs.last_stats()
     assert gs.debug_counters()[48] == 0 and st0.rays() == 0 and st0.box_tests == 0
-    for bad in ({"hot_copies": 3}, {"hot_copies": 128}, {"work_parts": 3}, {"counters": 2}):
+    # hot_copies: removed in round 6 (an unknown option is refused)
+    for bad in ({"hot_copies": 16}, {"work_parts": 3}, {"counters": 2}):
         with pytest.raises(rtamd.RTError):
             rtamd.render_scene("test7_s.txt", cwd=SCENES, options=bad)
 
@@ -1148,15 +1144,17 @@ def test_special_cases_on_the_bvh(cfg, accel, tmp_path):
 def test_deinterleave_rows_device(u8):
     """rt_deinterleave_rows (floats) and rt_deinterleave_rows_u8 (the
     writer's bytes) put gathered row sets (rth_row_set's dealing) back in
-    image order on the device, for ragged heights, several ranks, and row
+    image order on the device, for ragged heights, several ranks, row
     widths with and without the 16-B vector path (W * 3 * element bytes a
-    multiple of 16 or not)."""
+    multiple of 16 or not), and a tall narrow image (H > 65535)."""
     torch = pytest.importorskip("torch")
     import ctypes as C
     from rtamd.dist import image_rows, row_set
     L = rtamd.hip_lib()
     f = L.rt_deinterleave_rows_u8 if u8 else L.rt_deinterleave_rows
-    for H, world, W in ((67, 3, 13), (8, 2, 16), (130, 8, 13), (5, 1, 64), (41, 4, 48)):
+    # (70001 rows: taller than the grid's y extent, 65535 -- rows are
+    # grid-strided; round 5 refused such an image, ADVICE r5)
+    for H, world, W in ((67, 3, 13), (8, 2, 16), (130, 8, 13), (5, 1, 64), (41, 4, 48), (70001, 3, 1)):
         per = row_set(H, world, 0)[4]
         if u8:
             g = torch.randint(0, 256, (world, per, W, 3), dtype=torch.uint8, device="cuda:0")
@@ -1176,6 +1174,23 @@ def test_deinterleave_rows_device(u8):
         assert torch.equal(img, want), (H, world, W)
         assert f(C.c_void_p(g.data_ptr()), world, per - 1 if per > 1 else 0, W, H, 8,
                  C.c_void_p(img.data_ptr()), None) == -1
+
+
+def test_device_init_repeated():
+    """rt_device_init may be called again: a repeated call keeps at most one
+    waiting stream per device (each call used to add a stream, and
+    with it a hardware queue, to the pool) and scenes created after it render
+    the same image, stream reused or not."""
+    L = rtamd.hip_lib()
+    for _ in range(3):
+        assert L.rt_device_init(0) == 0
+    imgs = []
+    for _ in range(3):
+        img, st = rtamd.render_scene("test7_s.txt", cwd=SCENES)
+        imgs.append(img)
+    for img in imgs[1:]:
+        assert np.array_equal(np.nan_to_num(img, nan=-9), np.nan_to_num(imgs[0], nan=-9))
+    assert L.rt_device_init(-1) != 0
 
 
 @pytest.mark.parametrize("block", ["100000", "1", "7", "64"])

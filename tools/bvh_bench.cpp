@@ -3,11 +3,10 @@
 // bit for bit (rt_bvh.h Builder / quantize).  No GPU is used.
 //
 //   make -C simple-raytracer_amd bvh_bench
-//   simple-raytracer_amd/lib/bvh_bench scene.txt [threads] [reps] [hot_copies] [presplit]
+//   simple-raytracer_amd/lib/bvh_bench scene.txt [threads] [reps] [presplit]
 //
 // Prints one JSON line: primitives, nodes, per-phase ms (best of reps) for
-// the serial and the threaded build, "identical", and the check of a build
-// with hot copies of the tree's top (default 16) against the plain one.
+// the serial and the threaded build, "identical" and the tree's hash.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -44,66 +43,6 @@ static unsigned long long tree_hash(const AccelTree &t) {
     return h;
 }
 
-// Hot copies (AccelOpts::hot_copies): the tree read from copy c's root --
-// node bounds in DFS order and every leaf's record words -- must be the main
-// tree's, and the main arrays must be untouched by the copies.
-struct Walk {
-    const AccelTree &t;
-    unsigned long long h = 1469598103934665603ull;
-    bool bad = false;
-    void mix(const void *p, size_t n) {
-        const unsigned char *b = static_cast<const unsigned char *>(p);
-        for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
-    }
-    const rtbvh::NodeDev *node(int32_t link) {
-        const size_t nb = sizeof(rtbvh::NodeDev), off = (size_t)link;
-        if (t.hot_copies > 1 && off >= t.hot_base) {
-            const size_t c = (off - t.hot_base) / t.hot_stride, r = (off - t.hot_base) % t.hot_stride;
-            if (c >= (size_t)t.hot_copies || r % nb || r / nb >= (size_t)t.hot_per_copy) return nullptr;
-            return &t.hot_nodes[c * t.hot_per_copy + r / nb];
-        }
-        if (off % nb || off / nb >= (size_t)t.main_nodes) return nullptr;
-        return &t.nodes[off / nb];
-    }
-    void go(int32_t link, int depth) {
-        if (bad || depth > 200) { bad = true; return; }
-        if (link == rtbvh::kEmptyLeaf) { mix("e", 1); return; }
-        if (link < 0) {
-            int off, nfc, cnt;
-            rtbvh::leaf_decode(link, off, nfc, cnt);
-            const size_t words = 5 * (size_t)nfc + 2 * (size_t)(cnt - nfc);
-            if ((size_t)off + words + 3 > t.rec.size()) { bad = true; return; }
-            mix(&cnt, sizeof cnt);
-            mix(&t.rec[(size_t)off], words * sizeof(t.rec[0]));
-            return;
-        }
-        const rtbvh::NodeDev *z = node(link);
-        if (!z) { bad = true; return; }
-        mix(z, rtbvh::kNodeDevLinkOff);
-        for (int32_t l : z->link) go(l, depth + 1);
-    }
-};
-
-static bool hot_ok(const AccelTree &ref, const AccelTree &hot, int K, unsigned long long &walk_hash) {
-    const size_t nb = sizeof(rtbvh::NodeDev);
-    if (!hot.ok || hot.hot_copies != K || hot.nodes.size() != ref.nodes.size() ||
-        std::memcmp(hot.nodes.data(), ref.nodes.data(), ref.nodes.size() * nb) != 0 ||
-        hot.rec.size() < ref.rec.size() ||
-        std::memcmp(hot.rec.data(), ref.rec.data(), (ref.rec.size() - 3) * sizeof(ref.rec[0])) != 0 ||
-        hot.hot_base < ref.nodes.size() * nb || hot.hot_stride < (size_t)hot.hot_per_copy * nb ||
-        hot.hot_nodes.size() != (size_t)K * hot.hot_per_copy)
-        return false;
-    Walk m{ref};
-    m.go(0, 0);
-    walk_hash = m.h;
-    for (int c = 0; c < K; c++) {
-        Walk w{hot};
-        w.go((int32_t)(hot.hot_base + (size_t)c * hot.hot_stride), 0);
-        if (w.bad || w.h != m.h) return false;
-    }
-    return !m.bad;
-}
-
 int main(int argc, char **argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s scene.txt [threads] [reps]\n", argv[0]);
@@ -128,7 +67,7 @@ int main(int argc, char **argv) {
     accel_input(desc, in);
     const double input_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
     const double D = distance_bound(in, cam.eye);
-    const int presplit = argc > 5 ? std::atoi(argv[5]) : 0;
+    const int presplit = argc > 4 ? std::atoi(argv[4]) : 0;
     AccelTree ref, par;
     double best[2] = {1e30, 1e30}, ph[2][6];
     for (int r = 0; r < reps; r++) {
@@ -147,16 +86,6 @@ int main(int argc, char **argv) {
         }
     }
     const bool ident = same(ref, par);
-    // hot copies: built on the threaded path, checked against the plain tree
-    const int K = argc > 4 ? std::atoi(argv[4]) : 16;
-    AccelTree hot;
-    AccelOpts ho;
-    ho.threads = threads;
-    ho.hot_copies = K;
-    ho.presplit = presplit;
-    build_accel(in, D, ho, hot);
-    unsigned long long walk = 0;
-    const bool hot_good = !ref.ok || K < 2 || hot_ok(ref, hot, K, walk);
     auto phases = [&](int v) {
         static char b[2][256];
         std::snprintf(b[v], sizeof b[v],
@@ -168,13 +97,11 @@ int main(int argc, char **argv) {
     std::printf("{\"scene\": \"%s\", \"faces\": %d, \"spheres\": %d, \"lights\": %d, \"parse_ms\": %.3f, "
                 "\"input_ms\": %.3f, \"nodes\": %zu, \"main_nodes\": %lld, \"ok\": %d, \"threads\": %d, "
                 "\"serial_ms\": %.3f, \"threaded_ms\": %.3f, \"serial_phases_ms\": %s, \"threaded_phases_ms\": %s, "
-                "\"identical\": %s, \"hash\": \"%016llx\", \"hot_copies\": %d, \"hot_per_copy\": %d, "
-                "\"hot_records\": %zu, \"hot_ok\": %s, \"walk_hash\": \"%016llx\", \"node_bytes\": %zu, "
+                "\"identical\": %s, \"hash\": \"%016llx\", \"node_bytes\": %zu, "
                 "\"presplit\": %d, \"refs\": %lld, \"sah\": %.4f}\n",
                 argv[1], in.nf, in.ns, (int)in.lights.size(), parse_ms, input_ms, ref.nodes.size(), ref.main_nodes,
                 ref.ok ? 1 : 0, par.threads, best[0], best[1], phases(0), phases(1), ident ? "true" : "false", tree_hash(ref),
-                hot.hot_copies, hot.hot_per_copy, hot.rec.size() - ref.rec.size(), hot_good ? "true" : "false", walk,
                 sizeof(rtbvh::NodeDev), ref.presplit, ref.refs, ref.sah);
     rth_free(hs);
-    return ident && hot_good ? 0 : 3;
+    return ident ? 0 : 3;
 }

@@ -158,33 +158,6 @@ static int check_wide(const Result &R, const std::vector<Prim> &orig, int n, int
                     }
                 }
             }
-        // the 64-B nodes (8-bit planes, Node4Q): containment, an inverted box
-        // for every empty slot, and at most one quantisation step of slack
-        std::vector<Node4Q> Q8;
-        if (!quantize(Q4, Q8)) { printf("FAIL quantize8\n"); return 1; }
-        for (size_t k = 0; k < Q.nodes.size(); k++)
-            for (int a = 0; a < 3; a++) {
-                const double s = std::ldexp((double)Q8[k].scale[a], -24);
-                if (!(s > 0) || std::ldexp((double)Q8[k].scale[a], -24) * std::ldexp(1.0, 24) != Q8[k].scale[a]) {
-                    printf("FAIL quantize8 scale\n");
-                    return 1;
-                }
-                for (int i = 0; i < 4; i++) {
-                    const double l = node8_lo(Q8[k], a, i), h = node8_hi(Q8[k], a, i);
-                    if (Q4.nodes[k].link[i] == kEmpty || !(Q4.nodes[k].lo[a][i] <= Q4.nodes[k].hi[a][i])) {
-                        if (!(l > h)) { printf("FAIL quantize8 empty slot\n"); return 1; }
-                        continue;
-                    }
-                    if (!(l <= Q4.nodes[k].lo[a][i]) || !(h >= Q4.nodes[k].hi[a][i])) {
-                        printf("FAIL quantize8 containment\n");
-                        return 1;
-                    }
-                    if (Q4.nodes[k].lo[a][i] - l > s * (1 + 1e-9) || h - Q4.nodes[k].hi[a][i] > s * (1 + 1e-9)) {
-                        printf("FAIL quantize8 loose\n");
-                        return 1;
-                    }
-                }
-            }
     }
     // leaf record stream: same keys per leaf, faces first, contiguous words
     {
