@@ -10,7 +10,9 @@
 // --gpus N (rows dealt to N devices in 8-row blocks), --device D,
 // --gather host|rccl (how the devices' rows come together; host, the default:
 // each device copies its rows to the host; rccl: one RCCL gather to the first
-// device over xGMI, a device-side de-interleave and one copy to the host --
+// device over xGMI -- the writer's values as bytes, 3 B per pixel, or the
+// floats when a value is outside 0..255 -- a device-side de-interleave and
+// one copy to the host --
 // opt-in until a multi-device node has run tests/test_gpu_parity.py::
 // test_cli_rccl_gather_multi_device), --float-out FILE (raw float32 H*W*3
 // framebuffer), --stats, --stats-json FILE (the one-shot run's phases on
@@ -157,13 +159,23 @@ bool g_counters = false;
 // device-side de-interleave puts the rows in image order, one copy brings the
 // image to the host.  The seam is the reference's single render call
 // (main.cpp:607), its row loop (main.cpp:718) split across the devices.
+//
+// What crosses xGMI is the P3 writer's pixel values as bytes (3 B per pixel,
+// rt_quantize_u8 on each device; bench.py's gather does the same): a quarter
+// of the floats' bytes (C5 at N = 8: 101 MB per rank instead of 403).  When
+// some device flags a value outside 0..255 (NaN, a background above 1), or
+// the floats are wanted (want_floats: --float-out), the floats are gathered
+// instead.  bytes: true when img8 holds the image (write it with
+// rth_write_ppm_u8), false when img does.
 int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, int gpus, HostImage &img,
-                std::vector<rt_stats> &st) {
+                std::vector<unsigned char> &img8, bool want_floats, bool &bytes, std::vector<rt_stats> &st) {
     struct Dev {
         int id = 0;
         rt_scene *scene = nullptr;
         hipStream_t stream = nullptr;
         float *strip = nullptr, *recv = nullptr, *image = nullptr;
+        unsigned char *strip8 = nullptr, *recv8 = nullptr, *image8 = nullptr;
+        unsigned *flag = nullptr;
         int y0 = 0, step = 0, nrows = 0, rows_per = 0;
     };
     std::vector<Dev> d(gpus);
@@ -185,11 +197,16 @@ int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, i
         if (!e) set_counters(v.scene, g_counters);
         if (e) fail(rt_strerror(e), e);
         const size_t strip = (size_t)v.rows_per * W * 3 * sizeof(float);
+        const size_t strip8 = ((size_t)v.rows_per * W * 3 + 3) / 4 * 4;      // rt_quantize_u8: 4-B aligned
         if (!rc && (hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking) != hipSuccess ||
-                    hipMalloc(&v.strip, strip) != hipSuccess))
+                    hipMalloc(&v.strip, strip) != hipSuccess || hipMalloc(&v.strip8, strip8) != hipSuccess ||
+                    hipMalloc(&v.flag, sizeof(unsigned)) != hipSuccess ||
+                    hipMemsetAsync(v.flag, 0, sizeof(unsigned), v.stream) != hipSuccess))
             fail("device buffers", g);
         if (!rc && g == 0 && (hipMalloc(&v.recv, strip * gpus) != hipSuccess ||
-                              hipMalloc(&v.image, (size_t)W * H * 3 * sizeof(float)) != hipSuccess))
+                              hipMalloc(&v.image, (size_t)W * H * 3 * sizeof(float)) != hipSuccess ||
+                              hipMalloc(&v.recv8, strip8 * gpus) != hipSuccess ||
+                              hipMalloc(&v.image8, (size_t)W * H * 3) != hipSuccess))
             fail("gather buffers", g);
     }
     if (!rc) {
@@ -203,17 +220,46 @@ int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, i
             int e = rt_render_row_blocks_async(v.scene, &cam, W, H, v.y0, kRowBlock, v.step, v.nrows, v.strip,
                                                v.stream);
             if (e) fail(rt_strerror(e), e);
+            // the writer's values as bytes, on the device, after the render
+            if (!rc && !want_floats) {
+                e = rt_quantize_u8(v.strip, (long long)v.nrows * W * 3, v.strip8, v.flag, v.stream);
+                if (e) fail(rt_strerror(e), e);
+            }
         }
+    }
+    // every device's flag (4 bytes each): the bytes are the writer's only when
+    // no value anywhere is outside 0..255
+    bytes = !want_floats;
+    for (int g = 0; g < gpus && !rc && bytes; g++) {
+        unsigned f = 0;
+        (void)hipSetDevice(d[g].id);
+        if (hipMemcpyAsync(&f, d[g].flag, sizeof f, hipMemcpyDeviceToHost, d[g].stream) != hipSuccess ||
+            hipStreamSynchronize(d[g].stream) != hipSuccess)
+            fail("flag copy", g);
+        if (f & 1u) bytes = false;
     }
     if (!rc) {
         const size_t count = (size_t)d[0].rows_per * W * 3;
         ncclGroupStart();
-        for (int g = 0; g < gpus; g++)
-            ncclGather(d[g].strip, g == 0 ? d[0].recv : nullptr, count, ncclFloat32, 0, comms[g], d[g].stream);
+        for (int g = 0; g < gpus; g++) {
+            if (bytes)
+                ncclGather(d[g].strip8, g == 0 ? d[0].recv8 : nullptr, count, ncclUint8, 0, comms[g], d[g].stream);
+            else
+                ncclGather(d[g].strip, g == 0 ? d[0].recv : nullptr, count, ncclFloat32, 0, comms[g], d[g].stream);
+        }
         ncclResult_t r = ncclGroupEnd();
         if (r != ncclSuccess) fail(ncclGetErrorString(r), (int)r);
     }
-    if (!rc) {
+    if (!rc && bytes) {
+        (void)hipSetDevice(d[0].id);
+        int e = rt_deinterleave_rows_u8(d[0].recv8, gpus, d[0].rows_per, W, H, kRowBlock, d[0].image8, d[0].stream);
+        if (e) fail(rt_strerror(e), e);
+        img8.resize((size_t)W * H * 3);
+        if (!rc && (hipMemcpyAsync(img8.data(), d[0].image8, img8.size(), hipMemcpyDeviceToHost, d[0].stream) !=
+                        hipSuccess ||
+                    hipStreamSynchronize(d[0].stream) != hipSuccess))
+            fail("image copy", 0);
+    } else if (!rc) {
         (void)hipSetDevice(d[0].id);
         int e = rt_deinterleave_rows(d[0].recv, gpus, d[0].rows_per, W, H, kRowBlock, d[0].image, d[0].stream);
         if (e) fail(rt_strerror(e), e);
@@ -231,6 +277,10 @@ int render_rccl(rth_scene *hs, const rt_camera &cam, int W, int H, int device, i
         if (v.strip) (void)hipFree(v.strip);
         if (v.recv) (void)hipFree(v.recv);
         if (v.image) (void)hipFree(v.image);
+        if (v.strip8) (void)hipFree(v.strip8);
+        if (v.recv8) (void)hipFree(v.recv8);
+        if (v.image8) (void)hipFree(v.image8);
+        if (v.flag) (void)hipFree(v.flag);
         if (v.stream) (void)hipStreamDestroy(v.stream);
         if (v.scene) rt_scene_destroy(v.scene);
     }
@@ -336,9 +386,15 @@ int main(int argc, char *argv[]) {
     std::vector<rt_stats> st(gpus);
     std::vector<int> rcs(gpus, 0);
     std::vector<std::thread> pool;
+    std::vector<unsigned char> img8;      // --gather rccl: the writer's values as bytes, when they all fit
+    bool rccl_bytes = false;
     if (gather == "rccl") {
-        int r = render_rccl(hs, cam, W, H, device, gpus, img, st);
+        t = Clock::now();
+        int r = render_rccl(hs, cam, W, H, device, gpus, img, img8, float_out || std::getenv("RT_PPM_FLOATS"),
+                            rccl_bytes, st);
         if (r) return r;
+        ph_render = ms_since(t);
+        ppm_from = rccl_bytes ? "bytes" : "floats";
     }
     // --gather host: one host thread per device.  One device renders the image
     // in one call; several deal the rows out in 8-row blocks, round robin
@@ -464,7 +520,7 @@ int main(int argc, char *argv[]) {
     int wr = streamed_wr;
     if (!streamed) {
         t = Clock::now();
-        wr = rth_write_ppm(out, img.data(), W, H, 0);
+        wr = rccl_bytes ? rth_write_ppm_u8(out, img8.data(), W, H, 0) : rth_write_ppm(out, img.data(), W, H, 0);
         ph_write = ms_since(t);
     }
     if (wr != 0) {

@@ -203,27 +203,77 @@ def _render_on_device(path: str, cwd: str, depth: int):
     return img, st, hs, gs, cam
 
 
-def test_c4_full_size_row_sample(tmp_path):
+C4_ROWS, C4_PARTS = 64, 4             # C4's full-size sample: 64 rows, the oracle's work in 4 parts
+
+
+@pytest.fixture(scope="module")
+def c4_full(tmp_path_factory):
+    """BASELINE config C4 at its full 8192x8192 rendered whole into HBM by the
+    benched instantiation (counters = 0); C4_ROWS rows spread over the image
+    (one of them dense) read out for the parts below."""
+    torch = pytest.importorskip("torch")
+    d = str(tmp_path_factory.mktemp("c4"))
+    path = gen.write_scene(d, "C4")
+    hs = rtamd.HostScene(path, cwd=d)
+    W, H = hs.width, hs.height
+    cam = hs.camera()
+    gs = rtamd.GpuScene(hs)
+    gs.set_option("counters", 0)
+    img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+    gs.render_rows_async(cam, W, H, 0, H, img.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    gs.last_stats()
+    torch.cuda.synchronize()
+    assert gs.debug_counters()[48] == 0          # the uncounted (benched) instantiation ran
+    rows = np.unique(np.linspace(0, H - 1, C4_ROWS).astype(np.int32))
+    rows[1] = H // 3                             # the top rows are mostly sky: take a dense one too
+    rows = np.unique(rows)
+    got = img[rows.tolist()].cpu().numpy()
+    del img
+    gs.set_option("counters", 1)
+    ctx = dict(W=W, H=H, gs=gs, cam=cam, rows=rows, got=got, o=OracleScene(path, cwd=d), parts={})
+    yield ctx
+    parts = ctx["parts"].values()
+    _summary["C4_full_rows"] = dict(rows=int(sum(p["rows"] for p in parts)), pixels=int(sum(p["pixels"] for p in parts)),
+                                    max_abs=max((p["max_abs"] for p in parts), default=None), parts=len(parts),
+                                    sample={k: sum(p["sample"][k] for p in parts) for k in RAYS} if parts else {})
+    gs.close()
+
+
+@pytest.mark.parametrize("part", range(C4_PARTS))
+def test_c4_full_size_row_sample(c4_full, part):
     """BASELINE config C4 at its full 8192x8192: 10 000 textured triangles with
     the real-size 2048x1024 synthetic texture, a directional and a point light
-    (hard shadows).  Rendered by the benched instantiation (counters = 0); 8
-    rows across the image (one of them dense) against the oracle, with exact
-    per-type ray counts of those rows (main.cpp:718-764)."""
-    _, cnt = _benched_rows_vs_oracle(tmp_path, "C4", 8, key="C4_full_rows", dense_row=True)
+    (hard shadows), rendered by the benched instantiation (fixture c4_full).
+    Part `part` of its 64 sample rows (524 288 pixels in all) against the
+    oracle (on every CPU the lease grants: OMP_NUM_THREADS), and the same
+    rows' pixels rendered again by the counting instantiation
+    (rt_render_pixels): bit for bit the timed image's, with exactly the
+    oracle's per-type ray counts (main.cpp:718-764)."""
+    c = c4_full
+    n = (len(c["rows"]) + C4_PARTS - 1) // C4_PARTS
+    rows, got = c["rows"][part * n:(part + 1) * n], c["got"][part * n:(part + 1) * n]
+    ref, cnt = c["o"].render(rows=rows)
+    r = assert_parity(got, ref, f"C4 rows part {part} (counters=0)")
+    xs, ys = np.meshgrid(np.arange(c["W"], dtype=np.int32), rows)
+    xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
+    alone, st_px = c["gs"].render_pixels(c["cam"], c["W"], c["H"], xy)
+    assert np.array_equal(np.nan_to_num(alone.reshape(got.shape), nan=-9), np.nan_to_num(got, nan=-9))
+    assert _counts(st_px) == cnt, (_counts(st_px), cnt)
     assert cnt["shadow"] > 0
+    c["parts"][part] = dict(r, rows=int(len(rows)), pixels=int(len(xy)), sample=cnt)
 
 
 def test_c5_full_size_span_sample(tmp_path):
     """BASELINE config C5 at its full 16384x16384 with 100 000 spheres (depth 4,
-    the reference's): 64-pixel spans on 16 rows spread over the image against
-    the oracle (a full C5 row costs the oracle minutes).  The whole image is
-    rendered on the GPU first; the spans are read out of HBM."""
+    the reference's): 256-pixel spans on 64 rows spread over the image (16 384
+    pixels) against the oracle (a full C5 row costs the oracle minutes).  The
+    whole image is rendered on the GPU first; the spans are read out of HBM."""
     d = str(tmp_path)
     path = gen.write_scene(d, "C5")
     img, st, hs, gs, cam = _render_on_device(path, d, 4)
     W, H = hs.width, hs.height
     assert (W, H) == (16384, 16384) and st.primary == W * H
-    xy = _span_sample(W, H)
+    xy = _span_sample(W, H, rows=64, span=256)
     got = img[xy[:, 1].tolist(), xy[:, 0].tolist()].cpu().numpy()
     del img
     ref, cnt = OracleScene(path, cwd=d).render_pixels(W, H, xy)
@@ -256,19 +306,17 @@ def _ub_pixels(o: OracleScene, W: int, H: int, xy: np.ndarray) -> list:
     return out
 
 
-def test_c5_full_size_depth8_span_sample(tmp_path):
+C5D8_PARTS = 8                      # the depth-8 sample's oracle work in parts of 16 384 pixels
+
+
+@pytest.fixture(scope="module")
+def c5_depth8(tmp_path_factory):
     """BASELINE config C5 at its own setting: 16384x16384, 100 000 spheres,
-    reflection + refraction at DEPTH 8 (3.8 G rays).  The whole image is
-    rendered on the GPU into HBM; 16 384 pixels (128-pixel spans on 128
-    rows) are read out and compared with the oracle at depth 8 (pinned to
-    the reference's own depth-8 floats by ref_f/C5_32x32@d8 and C5_12x12@d8).
-    The same pixels rendered alone (rt_render_pixels) give bit for bit the
-    same colours and exactly the oracle's per-type ray counts.  Every pixel
-    of the frame whose shade tree reads back() of an empty medium stack
-    (main.cpp:1028: UB in the reference, defined here as eta_bkg like the
-    oracle) is listed by the kernel (rt_scene_debug_ub_pixels) and compared
-    with the oracle too; the list is in the summary (key C5_full_d8_spans)."""
-    d = str(tmp_path)
+    reflection + refraction at DEPTH 8 (3.8 G rays), rendered whole on the GPU
+    into HBM once; the 131 072 sample pixels (512-pixel spans on 256 rows)
+    and the pixels the kernel lists for back() of an empty medium stack are
+    read out for the tests below."""
+    d = str(tmp_path_factory.mktemp("c5d8"))
     path = gen.write_scene(d, "C5")
     img, st, hs, gs, cam = _render_on_device(path, d, 8)
     W, H = hs.width, hs.height
@@ -276,31 +324,62 @@ def test_c5_full_size_depth8_span_sample(tmp_path):
     events, ubxy = gs.debug_ub_pixels()
     assert events == st.ub_back
     ub_px = np.unique(ubxy, axis=0).astype(np.int32) if len(ubxy) else np.zeros((0, 2), np.int32)
-    xy = _span_sample(W, H, rows=128, span=128)
+    xy = _span_sample(W, H, rows=256, span=512)
     got = img[xy[:, 1].tolist(), xy[:, 0].tolist()].cpu().numpy()
     got_ub = img[ub_px[:, 1].tolist(), ub_px[:, 0].tolist()].cpu().numpy() if len(ub_px) else None
     del img
     o = OracleScene(path, cwd=d)
     o.set_depth(8)
-    ref, cnt = o.render_pixels(W, H, xy)
-    c = assert_parity(got, ref, "C5 depth 8 span sample")
-    alone, st_px = gs.render_pixels(cam, W, H, xy)
+    ctx = dict(W=W, H=H, gs=gs, cam=cam, st=st, xy=xy, got=got, ub_px=ub_px, got_ub=got_ub, events=int(events),
+               o=o, parts={})
+    yield ctx
+    tot = {k: sum(p["sample"][k] for p in ctx["parts"].values()) for k in RAYS + ("skip_trans", "ub_back")} \
+        if ctx["parts"] else {}
+    worst = max((p["max_abs"] for p in ctx["parts"].values()), default=None)
+    _summary["C5_full_d8_spans"] = dict(pixels=int(sum(p["pixels"] for p in ctx["parts"].values())),
+                                        parts=len(ctx["parts"]), max_abs=worst, gpu_total=_counts(st), sample=tot,
+                                        ub_back=ctx.get("ub"))
+    gs.close()
+
+
+@pytest.mark.parametrize("part", range(C5D8_PARTS))
+def test_c5_full_size_depth8_span_sample(c5_depth8, part):
+    """C5 at depth 8, full size (fixture c5_depth8): part `part` of the
+    131 072 sample pixels (16 384 each, so that no single test runs the
+    oracle for minutes) against the oracle at depth 8 (pinned to the
+    reference's own depth-8 floats by ref_f/C5_32x32@d8 and C5_12x12@d8).
+    The same pixels rendered alone (rt_render_pixels) give bit for bit the
+    whole image's colours and exactly the oracle's per-type ray counts."""
+    c = c5_depth8
+    n = len(c["xy"]) // C5D8_PARTS
+    xy, got = c["xy"][part * n:(part + 1) * n], c["got"][part * n:(part + 1) * n]
+    ref, cnt = c["o"].render_pixels(c["W"], c["H"], xy)
+    r = assert_parity(got, ref, f"C5 depth 8 span sample part {part}")
+    alone, st_px = c["gs"].render_pixels(c["cam"], c["W"], c["H"], xy)
     assert np.array_equal(np.nan_to_num(alone, nan=-9), np.nan_to_num(got, nan=-9))
     assert _counts(st_px) == cnt, (_counts(st_px), cnt)
     assert cnt["refraction"] > 0 and cnt["reflection"] > 0
-    ub = dict(events=int(events), pixels=int(len(ub_px)))
-    if len(ub_px):
-        # the UB pixels: the oracle defines the read as eta_bkg, like the kernel
-        ref_ub, cnt_ub = o.render_pixels(W, H, ub_px)
-        ub["parity"] = assert_parity(got_ub, ref_ub, "C5 depth 8 ub_back pixels")
-        alone_ub, st_ub = gs.render_pixels(cam, W, H, ub_px)
-        assert np.array_equal(np.nan_to_num(alone_ub, nan=-9), np.nan_to_num(got_ub, nan=-9))
+    c["parts"][part] = dict(r, pixels=int(len(xy)), sample=cnt)
+
+
+def test_c5_full_size_depth8_ub_pixels(c5_depth8):
+    """Every pixel of the depth-8 C5 frame whose shade tree reads back() of an
+    empty medium stack (main.cpp:1028: UB in the reference, defined here as
+    eta_bkg like the oracle) is listed by the kernel
+    (rt_scene_debug_ub_pixels) and compared with the oracle: agreement of two
+    restatements, parity-unpinned against the reference itself."""
+    c = c5_depth8
+    ub = dict(events=c["events"], pixels=int(len(c["ub_px"])))
+    if len(c["ub_px"]):
+        ref_ub, cnt_ub = c["o"].render_pixels(c["W"], c["H"], c["ub_px"])
+        ub["parity"] = assert_parity(c["got_ub"], ref_ub, "C5 depth 8 ub_back pixels")
+        alone_ub, st_ub = c["gs"].render_pixels(c["cam"], c["W"], c["H"], c["ub_px"])
+        assert np.array_equal(np.nan_to_num(alone_ub, nan=-9), np.nan_to_num(c["got_ub"], nan=-9))
         assert _counts(st_ub) == cnt_ub
-        if events <= 4096:                   # every event's pixel listed
-            assert cnt_ub["ub_back"] == events
-        ub["xy"] = ub_px.tolist()
-    _summary["C5_full_d8_spans"] = dict(c, pixels=len(xy), gpu_total=_counts(st), sample=cnt, ub_back=ub)
-    gs.close()
+        if c["events"] <= 4096:              # every event's pixel listed
+            assert cnt_ub["ub_back"] == c["events"]
+        ub["xy"] = c["ub_px"].tolist()
+    c["ub"] = ub
 
 
 def test_c2_full_size_whole_image(tmp_path):
@@ -1256,6 +1335,38 @@ def test_cli_rccl_gather(name, tmp_path):
     assert "rays primary=" in outs["rccl"][2]
 
 
+@pytest.mark.parametrize("name,want_from", [("C3_64x64.txt", "bytes"), ("edge_nested_nobkgeta.txt", "floats"),
+                                            ("test7_s.txt", None)])
+def test_cli_rccl_byte_gather_matches_host(name, want_from, tmp_path):
+    """`rt --gather rccl` gathers the P3 writer's values as bytes (3 B per
+    pixel, rt_quantize_u8 on each device) and falls back to the floats when
+    some value is outside 0..255 (edge_nested_nobkgeta: a background of 1.5
+    and -0.25): the PPM is byte for byte `--gather host`'s either way, and
+    --stats-json says which crossed the gather (main.cpp:718-719, the row
+    loop the gather reassembles)."""
+    import json as _json
+    outs, froms = {}, {}
+    for mode in ("host", "rccl"):
+        tmp_name = f"_cli8_{mode}_" + name
+        shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
+        ppm = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
+        sj = str(tmp_path / f"{mode}.json")
+        try:
+            r = subprocess.run([CLI, tmp_name, "--gpus", "1", "--gather", mode, "--stats-json", sj],
+                               cwd=SCENES, capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            outs[mode] = open(ppm, "rb").read()
+            froms[mode] = _json.load(open(sj))["ppm_from"]
+        finally:
+            for p in (os.path.join(SCENES, tmp_name), ppm):
+                if os.path.exists(p):
+                    os.remove(p)
+    assert len(outs["host"]) > 100 and outs["host"] == outs["rccl"]
+    assert froms["rccl"] == froms["host"], froms
+    if want_from:
+        assert froms["rccl"] == want_from, froms
+
+
 def _device_count() -> int:
     import ctypes as C
     return int(rtamd.hip_lib().rt_device_count())
@@ -1270,21 +1381,23 @@ def test_cli_rccl_gather_multi_device(tmp_path):
         pytest.skip("needs 2 HIP devices")
     name = "C3_64x64.txt"
     outs = {}
-    for mode in ("host", "rccl"):
+    # rccl8: without --float-out the gather carries the writer's bytes
+    for mode in ("host", "rccl", "rccl8"):
         tmp_name = f"_cli2_{mode}_" + name
         shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
         ppm = os.path.join(SCENES, tmp_name[:-4] + ".ppm")
         fout = str(tmp_path / f"{mode}.bin")
+        extra = [] if mode == "rccl8" else ["--float-out", fout]
         try:
-            r = subprocess.run([CLI, tmp_name, "--gpus", "2", "--gather", mode, "--float-out", fout],
+            r = subprocess.run([CLI, tmp_name, "--gpus", "2", "--gather", mode[:4]] + extra,
                                cwd=SCENES, capture_output=True, text=True, timeout=120)
             assert r.returncode == 0, r.stderr
-            outs[mode] = (open(ppm, "rb").read(), np.fromfile(fout, dtype=np.float32))
+            outs[mode] = (open(ppm, "rb").read(), np.fromfile(fout, dtype=np.float32) if extra else None)
         finally:
             for p in (os.path.join(SCENES, tmp_name), ppm):
                 if os.path.exists(p):
                     os.remove(p)
-    assert outs["host"][0] == outs["rccl"][0]
+    assert outs["host"][0] == outs["rccl"][0] == outs["rccl8"][0]
     assert np.array_equal(np.nan_to_num(outs["host"][1], nan=-9), np.nan_to_num(outs["rccl"][1], nan=-9))
 
 

@@ -5,8 +5,11 @@ alone, both as one frame (kernel clock) and pipelined the way bench.py runs
 N > 1 (frames in flight on the scene's render slots, block slots reserved for
 the gather).  The slowest rank bounds an N-GPU step; the projection assumes
 the ranks do not slow each other down (each has its own GPU) and adds the
-RCCL gather's xGMI time estimate (strip bytes / 153 GB/s per link, SURVEY.md
-§8e).  PROJECTED, not measured on N GPUs.
+RCCL gather: its cost on this GPU measured as a one-rank ncclGather of the
+strip (launch + local copy) and rank 0's quantise / de-interleave, plus the
+strip's bytes over one xGMI link (strip bytes / 153 GB/s: the N - 1 peers
+send over N - 1 links in parallel).  PROJECTED, not measured
+on N GPUs.
 
   python tools/rank_balance.py C3 [--frames 64] [--inflight 8] [--reserve 8]
 """
@@ -144,7 +147,7 @@ def main():
         launch_ms = timed(lambda: dist.gather(send, one, dst=0))
         del strip, send, gathered, image
         return dict(quantise_ms=round(q_ms, 4), deinterleave_ms=round(copy_ms, 4),
-                    gather_launch_ms=round(launch_ms, 4), total_ms=round(q_ms + copy_ms + launch_ms, 4))
+                    gather_one_rank_ms=round(launch_ms, 4), total_ms=round(q_ms + copy_ms + launch_ms, 4))
 
     base = None
     for n in (int(v) for v in a.ns.split(",")):
@@ -164,15 +167,16 @@ def main():
         k = [x["kernel_ms"] for x in ranks]
         p = [x["pipelined_ms"] for x in ranks]
         strip_bytes = row_set(H, n, 0)[4] * W * 3 * bpp
-        gather_ms = strip_bytes / (XGMI_GBPS * 1e9) * 1e3 if n > 1 else 0.0
+        xgmi_ms = strip_bytes / (XGMI_GBPS * 1e9) * 1e3 if n > 1 else 0.0
         # rank 0's extra work (quantise, de-interleave, the gather's launch)
         # counted whole, like the gather: it overlaps the next frames' renders
         # only partly
         extra = rank0_extra(n) if n > 1 else dict(total_ms=0.0)
-        step_ms = max(p) + gather_ms + extra["total_ms"]
+        step_ms = max(p) + xgmi_ms + extra["total_ms"]
         ent = dict(ranks=ranks, kernel_ms_max=max(k), kernel_ms_mean=round(sum(k) / n, 3),
                    balance=round(sum(k) / n / max(k), 3), pipelined_ms_max=max(p),
-                   gather_ms_est=round(gather_ms, 3), rank0_extra=extra, projected_step_ms=round(step_ms, 3),
+                   strip_bytes=strip_bytes, xgmi_ms=round(xgmi_ms, 4), rank0_extra=extra,
+                   projected_step_ms=round(step_ms, 3),
                    projected_Mrays_per_s=round(rays / step_ms / 1e3, 1))
         if base is None:
             base = ent["projected_Mrays_per_s"]
