@@ -686,14 +686,18 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
         RT_CSWAP(k2, c2, k3, c3);
         RT_CSWAP(k0, c0, k2, c2);
 #undef RT_CSWAP
-        stk[sp * kBlock] = c3;
-        sp += k3 != kMissKey ? 1 : 0;
-        stk[sp * kBlock] = c1;
-        sp += k1 != kMissKey ? 1 : 0;
-        stk[sp * kBlock] = c2;
-        sp += k2 != kMissKey ? 1 : 0;
-        stk[sp * kBlock] = c0;
-        sp += k0 != kMissKey ? 1 : 0;
+        // (only a lane with a B: another's top may be the LDS share's last
+        // entry, and a write above it would land in the lights)
+        if (has) {
+            stk[sp * kBlock] = c3;
+            sp += k3 != kMissKey ? 1 : 0;
+            stk[sp * kBlock] = c1;
+            sp += k1 != kMissKey ? 1 : 0;
+            stk[sp * kBlock] = c2;
+            sp += k2 != kMissKey ? 1 : 0;
+            stk[sp * kBlock] = c0;
+            sp += k0 != kMissKey ? 1 : 0;
+        }
     };
 #endif
     // The root (every trace starts there; wave-uniform) comes through scalar

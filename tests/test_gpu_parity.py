@@ -224,9 +224,10 @@ def c4_full(tmp_path_factory):
     gs.last_stats()
     torch.cuda.synchronize()
     assert gs.debug_counters()[48] == 0          # the uncounted (benched) instantiation ran
-    rows = np.unique(np.linspace(0, H - 1, C4_ROWS).astype(np.int32))
-    rows[1] = H // 3                             # the top rows are mostly sky: take a dense one too
-    rows = np.unique(rows)
+    # the top rows are mostly sky: one dense row besides (H // 3 + 1: no
+    # linspace row, so C4_ROWS + 1 rows in all)
+    rows = np.unique(np.append(np.linspace(0, H - 1, C4_ROWS).astype(np.int32), H // 3 + 1)).astype(np.int32)
+    assert len(rows) == C4_ROWS + 1
     got = img[rows.tolist()].cpu().numpy()
     del img
     gs.set_option("counters", 1)
@@ -244,7 +245,7 @@ def test_c4_full_size_row_sample(c4_full, part):
     """BASELINE config C4 at its full 8192x8192: 10 000 textured triangles with
     the real-size 2048x1024 synthetic texture, a directional and a point light
     (hard shadows), rendered by the benched instantiation (fixture c4_full).
-    Part `part` of its 64 sample rows (524 288 pixels in all) against the
+    Part `part` of its 65 sample rows (532 480 pixels in all) against the
     oracle (on every CPU the lease grants: OMP_NUM_THREADS), and the same
     rows' pixels rendered again by the counting instantiation
     (rt_render_pixels): bit for bit the timed image's, with exactly the

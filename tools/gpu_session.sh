@@ -4,7 +4,7 @@
 # fault or a timeout).  Usage:
 #   gpurun -- 'bash tools/gpu_session.sh NAME STEP [STEP ...]'
 # STEP: tests | bench[:CONFIG] | ab:CONFIG:ROUNDS:STEPS:SPEC,SPEC,... |
-#       prof:CONFIG | pmc:CONFIG[:LIBDIR] | e2e | phases:CONFIG[:OPTS] | balance:CONFIG[:NS] | cmd:NAME:CMD
+#       prof:CONFIG | overlap:CONFIG | pmc:CONFIG[:LIBDIR] | e2e | phases:CONFIG[:OPTS] | balance:CONFIG[:NS] | cmd:NAME:CMD
 set -o pipefail
 name=$1; shift
 out=gpurun_out/$name
@@ -27,6 +27,14 @@ for step in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof_$a" \
         -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config "$a" --steps 10 --warmup 2 --inflight 1 \
         --cpu-baseline off) > "$out/prof_$a.log" 2>&1 || { tail -20 "$out/prof_$a.log"; exit 1; } ;;
+    overlap)
+      # two frames in flight (bench.py's N = 1 setting) under a kernel trace:
+      # the dispatches' overlap and the period between their ends (the step)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$out/overlap_$a" \
+        -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --config "$a" --steps 20 --warmup 3 \
+        --inflight 2 --cpu-baseline off --count-render off) > "$out/overlap_$a.log" 2>&1 || { tail -20 "$out/overlap_$a.log"; exit 1; }
+      python3 tools/overlap_trace.py $(find "$out/overlap_$a" -name '*kernel_trace.csv' | head -1) --steps 20 \
+        > "$out/overlap_$a.json" 2>&1 || { tail -20 "$out/overlap_$a.json"; exit 1; } ;;
     pmc)
       # FETCH / WRITE bytes and the SQ/TA/TCC counters of one frame, one
       # rocprofv3 pass per counter group (never combined with tracing);
