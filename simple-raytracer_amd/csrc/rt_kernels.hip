@@ -291,7 +291,8 @@ typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plan
 #define RT_LEAF_WAIT 2
 #endif
 #ifndef RT_PAIR
-#define RT_PAIR 0          // 1: a traversal trip visits the stack top's inner node with the current one (A/B)
+#define RT_PAIR 0          // 1: a traversal trip visits the stack top's inner node with the current one,
+                           // 2: the same for any-hit searches only (A/B)
 #endif
 constexpr unsigned kLeafWait = RT_LEAF_WAIT;
 // The depth > 4 instantiation (MAXF 9/17: C5, depth 8, whose 100 000-sphere
@@ -739,7 +740,9 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
             int nb = node;
             if (!point) {
                 const int t = stk[(sp - 1) * kBlock];
-                pair = (t >= 0) & (sp - 1 <= p.stack_cap - 8);
+                // (RT_PAIR 2: any-hit searches only -- shadow rays and SKIP
+                // checks, whose visits do not depend on a running minimum)
+                pair = (t >= 0) & (sp - 1 <= p.stack_cap - 8) & (RT_PAIR == 1 || !q.closest);
                 nb = pair ? t : node;
                 sp -= pair ? 1 : 0;
             }
