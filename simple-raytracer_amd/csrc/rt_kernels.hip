@@ -290,10 +290,6 @@ typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plan
 #ifndef RT_LEAF_WAIT
 #define RT_LEAF_WAIT 2
 #endif
-#ifndef RT_PAIR
-#define RT_PAIR 0          // 1: a traversal trip visits the stack top's inner node with the current one,
-                           // 2: the same for any-hit searches only (A/B)
-#endif
 constexpr unsigned kLeafWait = RT_LEAF_WAIT;
 // The depth > 4 instantiation (MAXF 9/17: C5, depth 8, whose 100 000-sphere
 // tree is 12 levels deep) keeps descending until 12 lanes lack a leaf: C5
@@ -657,50 +653,6 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
             node = k0 != kMissKey ? pop_value(top1) : pop();
         }
     };
-#if RT_PAIR
-    // Paired trip (RT_PAIR): the stack top B, when it is an inner node, is
-    // visited in the same trip as the current node A -- two independent
-    // fetch -> planes -> keys chains per lane and trip.  B's hit children go
-    // on the stack first (its nearest on top of them), A's losers above,
-    // and the lane goes on with A's nearest child as before: every hit child
-    // is still visited (the order affects speed only).  Branch-free: a lane
-    // without a B reads A's node again (a cache hit) and its keys miss.
-    auto visit_b = [&](bool has, float4 w0, float4 wx, float4 wy, float4 wz, float4 w4) {
-        RT_COUNT(cnt.boxes += has ? 4u : 0u);
-        const float thi = thi_now();
-        int c0 = __float_as_int(w4.x), c1 = __float_as_int(w4.y), c2 = __float_as_int(w4.z), c3 = __float_as_int(w4.w);
-        const float4 wa[3] = {wx, wy, wz};
-        const ChildPlanes cp = child_planes(w0, wa, ix, iy, iz, ox, oy, oz);
-        unsigned k0 = has ? child_entry(cp, 0, tlo, thi) : kMissKey, k1 = has ? child_entry(cp, 1, tlo, thi) : kMissKey;
-        unsigned k2 = has ? child_entry(cp, 2, tlo, thi) : kMissKey, k3 = has ? child_entry(cp, 3, tlo, thi) : kMissKey;
-#define RT_CSWAP(ka, ca, kb, cb)                 \
-    {                                            \
-        bool sw = kb < ka;                       \
-        unsigned tk = sw ? kb : ka;              \
-        kb = sw ? ka : kb;                       \
-        ka = tk;                                 \
-        int tc = sw ? cb : ca;                   \
-        cb = sw ? ca : cb;                       \
-        ca = tc;                                 \
-    }
-        RT_CSWAP(k0, c0, k1, c1);
-        RT_CSWAP(k2, c2, k3, c3);
-        RT_CSWAP(k0, c0, k2, c2);
-#undef RT_CSWAP
-        // (only a lane with a B: another's top may be the LDS share's last
-        // entry, and a write above it would land in the lights)
-        if (has) {
-            stk[sp * kBlock] = c3;
-            sp += k3 != kMissKey ? 1 : 0;
-            stk[sp * kBlock] = c1;
-            sp += k1 != kMissKey ? 1 : 0;
-            stk[sp * kBlock] = c2;
-            sp += k2 != kMissKey ? 1 : 0;
-            stk[sp * kBlock] = c0;
-            sp += k0 != kMissKey ? 1 : 0;
-        }
-    };
-#endif
     // The root (every trace starts there; wave-uniform) comes through scalar
     // loads: the first step then has no vector-memory wait, which on gfx950
     // would also wait for every frame store the shading step just issued
@@ -733,33 +685,10 @@ __device__ void bvh_trace(Query &q, const Params &p, int *stk, CNT &cnt, bool or
             // node = the node's byte offset (rt_scene.cpp): five buffer loads
             // at immediate offsets from it; each axis window at the ray's
             // near-first offset (wo_*: 0 or 8 bytes, per lane)
-#if RT_PAIR
-            // B: the stack top when it is an inner node and its pushes (4) plus
-            // A's (3) fit the LDS share without a spill
-            bool pair = false;
-            int nb = node;
-            if (!point) {
-                const int t = stk[(sp - 1) * kBlock];
-                // (RT_PAIR 2: any-hit searches only -- shadow rays and SKIP
-                // checks, whose visits do not depend on a running minimum)
-                pair = (t >= 0) & (sp - 1 <= p.stack_cap - 8) & (RT_PAIR == 1 || !q.closest);
-                nb = pair ? t : node;
-                sp -= pair ? 1 : 0;
-            }
-#endif
             const float4 w0 = bld4(bvh_rs, node, 0), w4 = bld4(bvh_rs, node, rtbvh::kNodeLinkOff);
             const float4 wx = bld4(bvh_rs, node + wo_x, rtbvh::kNodeAxisOff);
             const float4 wy = bld4(bvh_rs, node + wo_y, rtbvh::kNodeAxisOff + 24);
             const float4 wz = bld4(bvh_rs, node + wo_z, rtbvh::kNodeAxisOff + 48);
-#if RT_PAIR
-            if (!point) {
-                const float4 v0 = bld4(bvh_rs, nb, 0), v4 = bld4(bvh_rs, nb, rtbvh::kNodeLinkOff);
-                const float4 vx = bld4(bvh_rs, nb + wo_x, rtbvh::kNodeAxisOff);
-                const float4 vy = bld4(bvh_rs, nb + wo_y, rtbvh::kNodeAxisOff + 24);
-                const float4 vz = bld4(bvh_rs, nb + wo_z, rtbvh::kNodeAxisOff + 48);
-                visit_b(pair, v0, vx, vy, vz, v4);
-            }
-#endif
 #if RT_PROF >= 2
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(w0.x), "v"(w4.x) : "memory");
             cnt.t_fetch += __builtin_amdgcn_s_memtime() - t_a;
