@@ -1356,60 +1356,77 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
         lds_load(h);
         const int phase = h_phase(h);
         if (phase == PH_LIGHT) {                     // main.cpp:952-958
-            const int light = h_light(h);
-            const ObjK &ob = row(p.objs, h.obj);
-            // the light's words in one batch (LightK: xyz w | col | L)
-            const LightW lw = light_words(p, light);
-            const f4v lw0 = lw.w0, lw1 = lw.w1, lw2 = lw.w2;
-            // L as light_vectors computed it for the shadow ray just traced:
-            // that ray's direction for a point light, the constant -L for a
-            // directional one (q.d is not modified by a trace)
-            V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
-            C3 lc = {lw1.x, lw1.y, lw1.z};
-            // the cumulative mask after this light: the earlier lights'
-            // times this light's factors (one product, reassociated)
-            const float mcum = clamp01(q.mask * prior_mask(q));
-            h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), phong_sum(h, ob, L)));
-            q.back = __float_as_int(mcum);
-            h.meta += 1u << 9;                       // next light
-            // stored at once, in the block that computed it: kept in registers
-            // across the other phases' code of the shading step, the colour
-            // was spilled to scratch and reloaded -- a reload whose vmcnt wait
-            // also waited for the frame stores of lanes that opened a child
-            lds_store_light(h);
-            if (light + 1 < p.nl) {
-                // next light's shadow ray from the same point: origin, self
-                // and cumulative mask are already in q (main.cpp:885-928)
-                // (opaque index: reusing this light's address for the next
-                // one kept a 64-bit pointer live -- and spilled -- across the
-                // shading code)
-                int next = light + 1;
-                asm volatile("" : "+v"(next));
-                // The node's last light, with a Phong sum of exactly 0: its
-                // term lc * mask * 0 is 0 whatever the ray meets, and its mask
-                // is not used after the light loop (main.cpp:788 starts the
-                // next node's at 1).  A prior mask of 0 makes the query a known
-                // one (counted, not searched) and its term 0 (Params::
-                // last_light_skip: finite light colours, no NaN factor).
-                // Tested before the query is set up, while the node's N, I
-                // and colour are still in registers.
-                bool zero = false;
+            // one light step per iteration (the loop continues only past known
+            // shadow rays, below)
+            for (;;) {
+                const int light = h_light(h);
+                const ObjK &ob = row(p.objs, h.obj);
+                // the light's words in one batch (LightK: xyz w | col | L)
+                const LightW lw = light_words(p, light);
+                const f4v lw0 = lw.w0, lw1 = lw.w1, lw2 = lw.w2;
+                // L as light_vectors computed it for the shadow ray just traced:
+                // that ray's direction for a point light, the constant -L for a
+                // directional one (q.d is not modified by a trace)
+                V3 L = lw0.w == 0.0f ? V3{lw2.x, lw2.y, lw2.z} : q.d;
+                C3 lc = {lw1.x, lw1.y, lw1.z};
+                // the cumulative mask after this light: the earlier lights'
+                // times this light's factors (one product, reassociated)
+                const float mcum = clamp01(q.mask * prior_mask(q));
+                h.acc = cadd(h.acc, cmulc(cmulf(lc, mcum), phong_sum(h, ob, L)));
+                q.back = __float_as_int(mcum);
+                h.meta += 1u << 9;                       // next light
+                // stored at once, in the block that computed it: kept in registers
+                // across the other phases' code of the shading step, the colour
+                // was spilled to scratch and reloaded -- a reload whose vmcnt wait
+                // also waited for the frame stores of lanes that opened a child
+                lds_store_light(h);
+                if (light + 1 >= p.nl) break;        // the light loop is done
+                {
+                    // next light's shadow ray from the same point: origin, self
+                    // and cumulative mask are already in q (main.cpp:885-928)
+                    // (opaque index: reusing this light's address for the next
+                    // one kept a 64-bit pointer live -- and spilled -- across the
+                    // shading code)
+                    int next = light + 1;
+                    asm volatile("" : "+v"(next));
+                    // The node's last light, with a Phong sum of exactly 0: its
+                    // term lc * mask * 0 is 0 whatever the ray meets, and its mask
+                    // is not used after the light loop (main.cpp:788 starts the
+                    // next node's at 1).  A prior mask of 0 makes the query a known
+                    // one (counted, not searched) and its term 0 (Params::
+                    // last_light_skip: finite light colours, no NaN factor).
+                    // Tested before the query is set up, while the node's N, I
+                    // and colour are still in registers.
+                    bool zero = false;
 #ifndef RT_LLSKIP
 #define RT_LLSKIP 1
 #endif
-                if (RT_LLSKIP && !kRecurse<MAXF> && p.last_light_skip && next == p.nl - 1) {
-                    const LightW nw = light_words(p, next);
-                    V3 Ln, sd;
-                    float dl;
-                    bool unb;
-                    light_vectors(nw, q.o, Ln, sd, dl, unb);   // Ln: the light step's L for either kind
-                    const C3 t = phong_sum(h, ob, Ln);
-                    zero = (t.r == 0.0f) & (t.g == 0.0f) & (t.b == 0.0f);
+                    if (RT_LLSKIP && !kRecurse<MAXF> && p.last_light_skip && next == p.nl - 1) {
+                        const LightW nw = light_words(p, next);
+                        V3 Ln, sd;
+                        float dl;
+                        bool unb;
+                        light_vectors(nw, q.o, Ln, sd, dl, unb);   // Ln: the light step's L for either kind
+                        const C3 t = phong_sum(h, ob, Ln);
+                        zero = (t.r == 0.0f) & (t.g == 0.0f) & (t.b == 0.0f);
+                    }
+                    shadow_query(q, p, next, h.obj);
+                    if (zero) q.back = __float_as_int(0.0f);
+                    // A known shadow ray (its prior mask is already 0, so its
+                    // cumulative mask stays 0 whatever it meets: render_kernel
+                    // counts it and does not search it): in the instantiation
+                    // without counters its light step is taken at once, in
+                    // this shading step, instead of after a trace step the
+                    // lane would sit out -- the same operations on the same
+                    // values (mask 1 from shadow_query times the prior 0; L
+                    // from the query just set up), so the same colour.  The
+                    // counting instantiation returns it, to count it.
+                    if constexpr (!std::remove_reference_t<decltype(cnt)>::kCount) {
+                        if (p.shadow_early_out && prior_mask(q) == 0.0f) continue;
+                    }
+                    ls.top = top;
+                    return RK_SHADOW;
                 }
-                shadow_query(q, p, next, h.obj);
-                if (zero) q.back = __float_as_int(0.0f);
-                ls.top = top;
-                return RK_SHADOW;
             }
         } else if (phase == PH_REFR) {
             if (q.skipped) {
