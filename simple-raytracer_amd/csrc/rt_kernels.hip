@@ -1415,13 +1415,19 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
                     // A known shadow ray (its prior mask is already 0, so its
                     // cumulative mask stays 0 whatever it meets: render_kernel
                     // counts it and does not search it): in the instantiation
-                    // without counters its light step is taken at once, in
-                    // this shading step, instead of after a trace step the
-                    // lane would sit out -- the same operations on the same
-                    // values (mask 1 from shadow_query times the prior 0; L
-                    // from the query just set up), so the same colour.  The
-                    // counting instantiation returns it, to count it.
-                    if constexpr (!std::remove_reference_t<decltype(cnt)>::kCount) {
+                    // without counters and without recursion (MAXF = 1) its
+                    // light step is taken at once, in this shading step,
+                    // instead of after a trace step the lane would sit out --
+                    // the same operations on the same values (mask 1 from
+                    // shadow_query times the prior 0; L from the query just
+                    // set up), so the same colour; the pixel then ends a step
+                    // sooner (C4 +1.5 %).  In the recursive instantiations the
+                    // lane would issue its reflection / refraction search a
+                    // step ahead of the wave's other lanes, which are still
+                    // tracing that light's shadow ray: C3 -2.4 %, C5 -2.1 %
+                    // (profiles/r06/ab/known_all_*.txt).  The counting
+                    // instantiation returns it, to count it.
+                    if constexpr (!std::remove_reference_t<decltype(cnt)>::kCount && !kRecurse<MAXF>) {
                         if (p.shadow_early_out && prior_mask(q) == 0.0f) continue;
                     }
                     ls.top = top;

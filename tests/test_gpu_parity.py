@@ -73,6 +73,19 @@ def test_scene_parity_forced_path(name, accel, golden):
     assert _counts(st) == cnt
 
 
+@pytest.mark.parametrize("accel", [0, 1])
+@pytest.mark.parametrize("name", golden_names(lambda v: v["width"] * v["height"] <= 300 * 300))
+def test_benched_instantiation_bit_identical(name, accel):
+    """The kernel instantiation bench.py times (option counters = 0) renders
+    every small fixture bit for bit like the counting one the parity tests pin
+    to the oracle, on both search paths -- including the shortcuts only it
+    takes (a known shadow ray's light step in the same shading step, round 6)."""
+    a, st_a = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel})
+    b, st_b = rtamd.render_scene(name, cwd=SCENES, options={"accel": accel, "counters": 0})
+    assert np.array_equal(np.nan_to_num(a, nan=-9), np.nan_to_num(b, nan=-9)), name
+    assert st_b.rays() == 0 and st_a.rays() > 0
+
+
 def test_strips_and_determinism():
     """Rendering rows in strips reproduces the full image bit for bit, and two
     renders are identical (no order dependence in the persistent scheduler)."""
