@@ -38,7 +38,7 @@ for step in "$@"; do
     pmc)
       # FETCH / WRITE bytes and the SQ/TA/TCC counters of one frame, one
       # rocprofv3 pass per counter group (never combined with tracing);
-      # b: a library variant's directory under simple-raytracer_amd/ (lib_n8)
+      # b: a library variant's directory under simple-raytracer_amd/ (lib_base)
       i=0; tag=$a${b:+_$b}
       if [ -n "$b" ]; then export RTAMD_LIB_DIR=$GRAFT_REPO_ROOT/simple-raytracer_amd/$b; else unset RTAMD_LIB_DIR; fi
       for pass in "FETCH_SIZE" "WRITE_SIZE" \
