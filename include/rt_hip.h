@@ -220,23 +220,6 @@ int rt_deinterleave_rows_u8(const unsigned char *gathered, int world, int rows_p
  * pixel instead of 12 (rtamd/dist.py ImageGather, bench.py). */
 int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *flag, void *hip_stream);
 
-/* The reference's P3 text (main.cpp:628-648: "P3 \n", "W H \n", "255 \n",
- * then per pixel "r g b \n", each value the std::to_string of the quantised
- * size_t of main.cpp:760) formatted on the device, byte for byte what
- * rth_write_ppm writes on the host.  values: W * H * 3 floats (kind
- * RT_P3_FLOAT: quantised as the writer does, NaN and out-of-range values
- * included) or the writer's values as bytes (RT_P3_U8: rt_quantize_u8 output),
- * device memory.  rt_p3_row_lengths writes each row's byte count to row_len[H]
- * (device); the caller forms row_off[H], the exclusive prefix sums (where each
- * row's text starts in `text`), and rt_format_p3_rows writes every row's text
- * there -- the pixel text only; the header (rth_ppm_open's) is the caller's.
- * Asynchronous on hip_stream.  The drop-in CLI formats on the device and
- * copies the text to the host (rt_cli.cpp write_ppm_device). */
-enum { RT_P3_FLOAT = 0, RT_P3_U8 = 1 };
-int rt_p3_row_lengths(const void *values, int kind, int W, int H, unsigned long long *row_len, void *hip_stream);
-int rt_format_p3_rows(const void *values, int kind, int W, int H, const unsigned long long *row_off, char *text,
-                      void *hip_stream);
-
 /* Kernel selection / tuning knobs: "accel" (-1 auto, 0 brute-force scan,
  * 1 BVH), "lds" (-1 auto, 0/1: stage the scan's scene in LDS), "grid"
  * (persistent blocks, 0 = occupancy), "reserve" (block slots the occupancy-

@@ -13,8 +13,6 @@
 #ifndef RT_HOST_H
 #define RT_HOST_H
 
-#include <stddef.h>
-
 #include "rt_hip.h"
 
 #ifdef __cplusplus
@@ -63,10 +61,6 @@ int rth_write_ppm(const char *path, const float *rgb, int W, int H, int threads)
 typedef struct rth_ppm_stream rth_ppm_stream;
 int rth_ppm_open(const char *path, int W, int H, int threads, rth_ppm_stream **out);
 int rth_ppm_write_rows(rth_ppm_stream *stream, const float *rgb, int nrows);
-/* Append n bytes of pixel text that is already formatted (rt_format_p3_rows
- * output copied to the host) and count nrows more rows as written: the
- * stream's threads pwrite it in pieces.  0 or -1. */
-int rth_ppm_write_text(rth_ppm_stream *stream, const char *text, size_t n, int nrows);
 int rth_ppm_close(rth_ppm_stream *stream);
 
 /* The same file from the pixel values as bytes (W * H * 3, or nrows * W * 3

@@ -149,93 +149,6 @@ int write_ppm_bytes(const char *path, const float *dimg, int W, int H, int &hip_
     return ret;
 }
 
-// One device, P3 out formatted on the device (rt_p3_row_lengths +
-// rt_format_p3_rows: the reference's writer, main.cpp:628-648, byte for byte
-// rth_write_ppm's, every value kind included): the rows' text lengths come to
-// the host (8 B per row) for their offsets, the text is formatted into HBM and
-// copied to the host -- in one pageable copy below kStreamText bytes, else in
-// 64-MB pieces through two pinned buffers, each written (rth_ppm_write_text:
-// the writer's threads pwrite it) while the next one copies.  The host does no
-// formatting: C3's 178 MB of text cost the writer's 16 threads ~25 ms.
-// Returns 0, or -1 on a write error; a HIP error goes to hip_rc.  d2h_ms: the
-// pageable copy (0 when streamed: overlapped with the write); fmt_ms: the
-// device formatting, offsets included.
-int write_ppm_device(const char *path, const void *dvals, int kind, int W, int H, int &hip_rc, double &d2h_ms,
-                     double &fmt_ms) {
-    const auto t0 = Clock::now();
-    unsigned long long *drow = nullptr;
-    char *dtext = nullptr;
-    std::vector<unsigned long long> off((size_t)H);
-    size_t total = 0;
-    if (hipMalloc((void **)&drow, (size_t)H * sizeof(unsigned long long)) != hipSuccess ||
-        rt_p3_row_lengths(dvals, kind, W, H, drow, nullptr) != RT_OK ||
-        hipMemcpy(off.data(), drow, off.size() * sizeof(off[0]), hipMemcpyDeviceToHost) != hipSuccess)
-        hip_rc = RT_E_HIP;
-    for (size_t y = 0; !hip_rc && y < off.size(); y++) {
-        const size_t n = off[y];
-        off[y] = total;
-        total += n;
-    }
-    if (!hip_rc && (hipMalloc((void **)&dtext, std::max<size_t>(1, total)) != hipSuccess ||
-                    hipMemcpy(drow, off.data(), off.size() * sizeof(off[0]), hipMemcpyHostToDevice) != hipSuccess ||
-                    rt_format_p3_rows(dvals, kind, W, H, drow, dtext, nullptr) != RT_OK ||
-                    hipDeviceSynchronize() != hipSuccess))
-        hip_rc = RT_E_HIP;
-    fmt_ms = ms_since(t0);
-    int ret = -1;
-    rth_ppm_stream *ps = nullptr;
-    size_t chunk = size_t(64) << 20;
-    if (const char *e = std::getenv("RT_PPM_TEXT_CHUNK")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10));  // test hook
-    const bool stream = total >= (size_t(512) << 20) || std::getenv("RT_PPM_TEXT_CHUNK") != nullptr;
-    if (!hip_rc && rth_ppm_open(path, W, H, 0, &ps) == 0) {
-        bool good = true;
-        if (!stream) {
-            std::unique_ptr<char[]> host(new char[std::max<size_t>(1, total)]);
-            const auto t1 = Clock::now();
-            if (hipMemcpy(host.get(), dtext, total, hipMemcpyDeviceToHost) != hipSuccess) hip_rc = RT_E_HIP;
-            d2h_ms = ms_since(t1);
-            good = !hip_rc && rth_ppm_write_text(ps, host.get(), total, H) == 0;
-        } else {
-            char *pin[2] = {nullptr, nullptr};
-            hipStream_t cs = nullptr;
-            hipEvent_t ev[2] = {nullptr, nullptr};
-            const size_t nb = (total + chunk - 1) / chunk;
-            if (hipHostMalloc((void **)&pin[0], std::min(chunk, total), hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&pin[1], std::min(chunk, total), hipHostMallocDefault) != hipSuccess ||
-                hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess)
-                hip_rc = RT_E_HIP;
-            auto len = [&](size_t b) { return std::min(chunk, total - b * chunk); };
-            auto issue = [&](size_t b) {
-                if (hipMemcpyAsync(pin[b & 1], dtext + b * chunk, len(b), hipMemcpyDeviceToHost, cs) != hipSuccess ||
-                    hipEventRecord(ev[b & 1], cs) != hipSuccess)
-                    hip_rc = RT_E_HIP;
-            };
-            if (!hip_rc && nb > 0) issue(0);
-            for (size_t b = 0; !hip_rc && b < nb; b++) {
-                if (b + 1 < nb) issue(b + 1);          // into the buffer piece b - 1 has left
-                if (hip_rc || hipEventSynchronize(ev[b & 1]) != hipSuccess) {
-                    hip_rc = RT_E_HIP;
-                    break;
-                }
-                if (rth_ppm_write_text(ps, pin[b & 1], len(b), b + 1 == nb ? H : 0) != 0) good = false;
-            }
-            if (nb == 0 && rth_ppm_write_text(ps, nullptr, 0, H) != 0) good = false;
-            if (cs) (void)hipStreamSynchronize(cs);
-            for (int k = 0; k < 2; k++) {
-                if (pin[k]) (void)hipHostFree(pin[k]);
-                if (ev[k]) (void)hipEventDestroy(ev[k]);
-            }
-            if (cs) (void)hipStreamDestroy(cs);
-            d2h_ms = 0.0;
-        }
-        ret = rth_ppm_close(ps) == 0 && good && !hip_rc ? 0 : -1;
-    }
-    if (drow) (void)hipFree(drow);
-    if (dtext) (void)hipFree(dtext);
-    return ret;
-}
-
 // The kernel instantiation with counters (rays by kind, executed tests)
 // only when the run reports them (--stats, --stats-json): ~4 % slower
 void set_counters(rt_scene *s, bool on) { (void)rt_scene_set_option(s, "counters", on ? 1 : 0); }
@@ -401,7 +314,6 @@ int main(int argc, char *argv[]) {
     }
     // phases of the one-shot run (--stats-json), host clock
     double ph_parse = 0, ph_create = 0, ph_bvh = 0, ph_render = 0, ph_d2h = 0, ph_write = 0;
-    double ph_fmt = 0;                     // device P3 formatting (inside ph_write)
     // The HIP runtime and the device's context start on a thread of their
     // own while the scene file is parsed (C5's 11 MB: ~35 ms, HIP's start
     // 50-130 ms): neither needs the other
@@ -506,28 +418,14 @@ int main(int argc, char *argv[]) {
         if (!r) r = rt_render_rows(s, &cam, W, H, 0, H, dimg, &st[0]);
         ph_render = ms_since(t);
         t = Clock::now();
-        // the P3 text formatted on the device and copied to the host
-        // (write_ppm_device), unless --float-out wants the floats; RT_PPM_HOST
-        // selects the host formatting paths below (A/B, tests)
-        bool device_text = false;
-        if (!r && !float_out && !std::getenv("RT_PPM_HOST")) {
-            double d2h = 0.0;
-            streamed_wr = write_ppm_device(out, dimg, RT_P3_FLOAT, W, H, r, d2h, ph_fmt);
-            streamed = true;
-            device_text = true;
-            ph_d2h = d2h;
-            ph_write = ms_since(t) - d2h;
-            d2h_overlapped = d2h == 0.0;
-        }
-        t = Clock::now();
-        // host formatting (RT_PPM_HOST): below 512 MB of floats the writer's
-        // values as bytes, quantised on the device (3 B per pixel to the
-        // host); the floats when some value is not 0..255, or --float-out
-        // wants them, or the image is large enough for the pinned
-        // copy-and-write overlap below (C4, C5: it hides the copy entirely)
+        // below 512 MB of floats: the writer's values as bytes, quantised on
+        // the device (3 B per pixel to the host); the floats when some value
+        // is not 0..255, or --float-out wants them, or the image is large
+        // enough for the pinned copy-and-write overlap below (C4, C5: it
+        // hides the copy entirely)
         const bool big = (size_t)W * H * 3 * sizeof(float) >= (size_t(512) << 20);
         int bytes_rc = 1;
-        if (!r && !streamed && !float_out && !big && !std::getenv("RT_PPM_FLOATS")) {
+        if (!r && !float_out && !big && !std::getenv("RT_PPM_FLOATS")) {
             double d2h = 0.0;
             bytes_rc = write_ppm_bytes(out, dimg, W, H, r, d2h);
             if (bytes_rc != 1) {           // written (or failed): one phase, reported as the write
@@ -556,7 +454,7 @@ int main(int argc, char *argv[]) {
                 r = RT_E_HIP;
             ph_d2h = ms_since(t);
         }
-        ppm_from = device_text ? "device text" : bytes_rc == 1 ? "floats" : "bytes";
+        ppm_from = bytes_rc == 1 ? "floats" : "bytes";
         // --stats / --stats-json: the counts from one more render by the
         // counting instantiation, outside the phases (its image is the same)
         if (!r && g_counters) {
@@ -654,11 +552,11 @@ int main(int argc, char *argv[]) {
                     "\"rays\": %llu, \"hip_init_thread_ms\": %.3f, \"phases_ms\": {\"parse\": %.3f, \"hip_init\": %.3f, \"host_image_alloc\": %.3f, "
                     "\"scene_upload\": %.3f, \"bvh_build\": %.3f, "
                     "\"bvh_build_host\": %.3f, \"render\": %.3f, \"kernel\": %.3f, \"d2h\": %.3f, "
-                    "\"quantise_ppm_write\": %.3f, \"p3_format_device\": %.3f}, \"d2h_overlapped_with_write\": %s, \"ppm_from\": \"%s\", \"count_render_ms\": %.3f, "
+                    "\"quantise_ppm_write\": %.3f}, \"d2h_overlapped_with_write\": %s, \"ppm_from\": \"%s\", \"count_render_ms\": %.3f, "
                     "\"total_ms\": %.3f, \"ppm_bytes\": %lld, "
                     "\"Mrays_per_s_end_to_end\": %.3f, \"Mrays_per_s_kernel\": %.3f}\n",
                     argv[1], W, H, eff_depth, gpus, gather.c_str(), rays, init_ms, ph_parse, ph_hip_init, ph_alloc, ph_create, ph_bvh, bvh_host, ph_render,
-                    kms, ph_d2h, ph_write, ph_fmt, d2h_overlapped ? "true" : "false", ppm_from, ph_count, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
+                    kms, ph_d2h, ph_write, d2h_overlapped ? "true" : "false", ppm_from, ph_count, total, ppm_bytes, rays / (total * 1e3), kms > 0 ? rays / (kms * 1e3) : 0.0);
             if (f != stderr) fclose(f);
         }
     }

@@ -262,13 +262,6 @@ hipError_t quantize_u8_launch(const float *rgb, size_t n, unsigned char *out, un
 // tests; option counters; rt_kernels.hip RT_COUNT)
 hipError_t render_launch(int maxf, int mode, bool count, const Params &p, unsigned grid, size_t lds_bytes,
                          hipStream_t st);
-// The P3 writer's text on the device (rt_p3_row_lengths / rt_format_p3_rows):
-// vals = W * H * 3 floats (u8 = false) or the writer's bytes (u8 = true);
-// row_len[y] = bytes of row y's text; row_off[y] = its offset in text
-hipError_t p3_row_lengths_launch(const void *vals, bool u8, int W, int H, unsigned long long *row_len,
-                                 hipStream_t st);
-hipError_t p3_format_launch(const void *vals, bool u8, int W, int H, const unsigned long long *row_off, char *text,
-                            hipStream_t st);
 // gathered row sets -> image order; a row is row_bytes bytes of elements of
 // elem_bytes (4: floats, 1: the writer's bytes)
 hipError_t deinterleave_launch(const void *gathered, size_t row_bytes, size_t elem_bytes, int world, int rows_per,

@@ -769,37 +769,6 @@ int rth_write_ppm_u8(const char *path, const unsigned char *v, int W, int H, int
     return (rth_ppm_close(st) == 0 && rc == 0) ? 0 : -1;
 }
 
-int rth_ppm_write_text(rth_ppm_stream *st, const char *text, size_t n, int nrows) {
-    if (!st || (!text && n > 0) || nrows < 0 || st->rows + nrows > st->H) return -1;
-    // already formatted (rt_format_p3_rows on the device): the bytes go to
-    // the file at the stream's offset, in pieces of at least 4 MB pwritten by
-    // the stream's threads at once (a single writer moves ~1-2 GB/s into the
-    // page cache)
-    const size_t piece = std::max<size_t>(size_t(4) << 20, (n + (size_t)st->threads - 1) / (size_t)st->threads);
-    const size_t np = n == 0 ? 0 : (n + piece - 1) / piece;
-    std::atomic<bool> good{true};
-    auto put = [&](size_t k) {
-        const size_t a = k * piece, e = std::min(n, a + piece);
-        size_t done = 0;
-        while (a + done < e) {
-            const ssize_t w = ::pwrite(st->fd, text + a + done, e - a - done, (off_t)(st->off + a + done));
-            if (w <= 0) {
-                good = false;
-                return;
-            }
-            done += (size_t)w;
-        }
-    };
-    std::vector<std::thread> pool;
-    for (size_t k = 1; k < np; k++) pool.emplace_back(put, k);
-    if (np) put(0);
-    for (auto &th : pool) th.join();
-    st->off += n;
-    st->rows += nrows;
-    if (!good) st->good = false;
-    return good ? 0 : -1;
-}
-
 int rth_ppm_close(rth_ppm_stream *st) {
     if (!st) return -1;
     bool good = st->good && st->rows == st->H;

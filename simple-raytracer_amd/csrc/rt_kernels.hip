@@ -2027,137 +2027,6 @@ hipError_t quantize_u8_launch(const float *rgb, size_t n, unsigned char *out, un
 }
 
 // ---------------------------------------------------------------------------
-// The P3 text on the device (rt_p3_row_lengths / rt_format_p3_rows): the
-// reference's writer, main.cpp:628-648 -- per pixel "r g b \n", each value the
-// std::to_string of the quantised size_t (main.cpp:760: static_cast<int> of
-// map(c, 0, 1, 0, 255), INT_MIN for NaN and out-of-range floats, a negative
-// int converted to size_t), exactly as rth_quantize / rth_ppm_write_rows
-// format it on the host.  Values come as floats (the image) or as the writer's
-// bytes (rt_quantize_u8 output: every value 0..255).  One workgroup per row;
-// a row's pixels are formatted in chunks of the workgroup's size, each lane
-// writing its pixel's text at its prefix-summed offset.
-// ---------------------------------------------------------------------------
-constexpr int kP3Block = 256;
-
-// the writer's value of float c (rt_host.cpp quantize1, the same operations)
-__device__ __forceinline__ unsigned long long p3_value(float c) {
-    const float x = (c - 0.0f) * (255.0f - 0.0f) / (1.0f - 0.0f) + 0.0f;
-    const long long v = (x >= -2147483648.0f && x < 2147483648.0f) ? (long long)(int)x : (long long)INT_MIN;
-    return (unsigned long long)v;
-}
-__device__ __forceinline__ int p3_digits(unsigned long long v) {
-    if (v < 10ull) return 1;
-    if (v < 100ull) return 2;
-    if (v < 1000ull) return 3;
-    int n = 3;
-    for (unsigned long long t = v / 1000ull; t; t /= 10ull) n++;
-    return n;
-}
-template <bool U8>
-__device__ __forceinline__ unsigned long long p3_elem(const void *vals, size_t i) {
-    if constexpr (U8)
-        return static_cast<const unsigned char *>(vals)[i];
-    else
-        return p3_value(static_cast<const float *>(vals)[i]);
-}
-// bytes of pixel (x, y)'s text: three values and a space after each, '\n'
-template <bool U8>
-__device__ __forceinline__ unsigned p3_pixel_len(const void *vals, size_t i3, unsigned long long &a,
-                                                 unsigned long long &b, unsigned long long &c) {
-    a = p3_elem<U8>(vals, i3), b = p3_elem<U8>(vals, i3 + 1), c = p3_elem<U8>(vals, i3 + 2);
-    return (unsigned)(p3_digits(a) + p3_digits(b) + p3_digits(c) + 4);
-}
-__device__ __forceinline__ char *p3_put(char *o, unsigned long long v) {
-    const int n = p3_digits(v);
-    for (int k = n - 1; k >= 0; k--) {
-        o[k] = (char)('0' + (int)(v % 10ull));
-        v /= 10ull;
-    }
-    o[n] = ' ';
-    return o + n + 1;
-}
-template <bool U8>
-__global__ void __launch_bounds__(kP3Block) p3_row_len_kernel(const void *__restrict__ vals, int W, int H,
-                                                              unsigned long long *__restrict__ row_len) {
-    __shared__ unsigned long long part[kP3Block / 64];
-    for (int y = blockIdx.x; y < H; y += gridDim.x) {
-        unsigned long long n = 0;
-        for (int x = threadIdx.x; x < W; x += kP3Block) {
-            unsigned long long a, b, c;
-            n += p3_pixel_len<U8>(vals, ((size_t)y * W + x) * 3, a, b, c);
-        }
-        for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x / 64] = n;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long t = 0;
-            for (int w = 0; w < kP3Block / 64; w++) t += part[w];
-            row_len[y] = t;
-        }
-        __syncthreads();
-    }
-}
-template <bool U8>
-__global__ void __launch_bounds__(kP3Block) p3_format_kernel(const void *__restrict__ vals, int W, int H,
-                                                             const unsigned long long *__restrict__ row_off,
-                                                             char *__restrict__ text) {
-    __shared__ unsigned wsum[kP3Block / 64];
-    for (int y = blockIdx.x; y < H; y += gridDim.x) {
-        unsigned long long base = row_off[y];
-        for (int x0 = 0; x0 < W; x0 += kP3Block) {
-            const int x = x0 + (int)threadIdx.x;
-            unsigned long long a = 0, b = 0, c = 0;
-            const unsigned len = x < W ? p3_pixel_len<U8>(vals, ((size_t)y * W + x) * 3, a, b, c) : 0u;
-            // exclusive prefix sum of len over the workgroup: within the wave
-            // by shuffles, then the waves' totals
-            const int lane = (int)(threadIdx.x & 63);
-            unsigned inc = len;
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned t = __shfl_up(inc, o);
-                if (lane >= o) inc += t;
-            }
-            if (lane == 63) wsum[threadIdx.x / 64] = inc;
-            __syncthreads();
-            unsigned before = 0, total = 0;
-            for (int w = 0; w < kP3Block / 64; w++) {
-                const unsigned t = wsum[w];
-                before += w < (int)(threadIdx.x / 64) ? t : 0u;
-                total += t;
-            }
-            if (x < W) {
-                char *o = text + base + before + (inc - len);
-                o = p3_put(o, a);
-                o = p3_put(o, b);
-                o = p3_put(o, c);
-                *o = '\n';
-            }
-            base += total;
-            __syncthreads();                         // wsum is rewritten by the next chunk
-        }
-    }
-}
-
-hipError_t p3_row_lengths_launch(const void *vals, bool u8, int W, int H, unsigned long long *row_len,
-                                 hipStream_t st) {
-    const unsigned grid = (unsigned)std::min(H, 8192);
-    if (u8)
-        hipLaunchKernelGGL(p3_row_len_kernel<true>, dim3(grid), dim3(kP3Block), 0, st, vals, W, H, row_len);
-    else
-        hipLaunchKernelGGL(p3_row_len_kernel<false>, dim3(grid), dim3(kP3Block), 0, st, vals, W, H, row_len);
-    return hipGetLastError();
-}
-
-hipError_t p3_format_launch(const void *vals, bool u8, int W, int H, const unsigned long long *row_off, char *text,
-                            hipStream_t st) {
-    const unsigned grid = (unsigned)std::min(H, 8192);
-    if (u8)
-        hipLaunchKernelGGL(p3_format_kernel<true>, dim3(grid), dim3(kP3Block), 0, st, vals, W, H, row_off, text);
-    else
-        hipLaunchKernelGGL(p3_format_kernel<false>, dim3(grid), dim3(kP3Block), 0, st, vals, W, H, row_off, text);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // Launch interface (rt_device.h)
 // ---------------------------------------------------------------------------
 int maxf_for_depth(int depth) {

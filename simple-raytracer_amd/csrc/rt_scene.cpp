@@ -846,22 +846,6 @@ int rt_deinterleave_rows_u8(const unsigned char *gathered, int world, int rows_p
     return deinterleave(gathered, 1, world, rows_per, W, H, block, image, hip_stream);
 }
 
-int rt_p3_row_lengths(const void *values, int kind, int W, int H, unsigned long long *row_len, void *hip_stream) {
-    if (!values || !row_len || W < 1 || H < 1 || (kind != RT_P3_FLOAT && kind != RT_P3_U8)) return RT_E_INVALID;
-    return p3_row_lengths_launch(values, kind == RT_P3_U8, W, H, row_len, (hipStream_t)hip_stream) == hipSuccess
-               ? RT_OK
-               : RT_E_HIP;
-}
-
-int rt_format_p3_rows(const void *values, int kind, int W, int H, const unsigned long long *row_off, char *text,
-                      void *hip_stream) {
-    if (!values || !row_off || !text || W < 1 || H < 1 || (kind != RT_P3_FLOAT && kind != RT_P3_U8))
-        return RT_E_INVALID;
-    return p3_format_launch(values, kind == RT_P3_U8, W, H, row_off, text, (hipStream_t)hip_stream) == hipSuccess
-               ? RT_OK
-               : RT_E_HIP;
-}
-
 int rt_quantize_u8(const float *rgb, long long n, unsigned char *out, unsigned *flag, void *hip_stream) {
     if (!rgb || !out || !flag || n < 0) return RT_E_INVALID;
     if ((reinterpret_cast<uintptr_t>(rgb) & 15) || (reinterpret_cast<uintptr_t>(out) & 3)) return RT_E_INVALID;

@@ -87,13 +87,13 @@ _hip = None
 HOST_SYMBOLS = ["rth_parse_file", "rth_free", "rth_desc", "rth_set_depth", "rth_set_imsize",
                 "rth_width", "rth_height", "rth_camera", "rth_quantize", "rth_write_ppm",
                 "rth_output_path", "rth_row_set", "rth_ppm_open", "rth_ppm_write_rows", "rth_ppm_close",
-                "rth_write_ppm_u8", "rth_ppm_write_rows_u8", "rth_ppm_write_text"]
+                "rth_write_ppm_u8", "rth_ppm_write_rows_u8"]
 HIP_SYMBOLS = ["rt_device_count", "rt_device_init", "rt_scene_create", "rt_scene_destroy", "rt_render_rows",
                "rt_render_rows_async", "rt_render_row_blocks_async", "rt_render_row_blocks", "rt_render_pixels",
                "rt_scene_last_stats", "rt_scene_prepare",
                "rt_scene_set_option", "rt_scene_debug_counters", "rt_scene_debug_wavelog", "rt_scene_debug_ub_pixels",
                "rt_deinterleave_rows", "rt_deinterleave_rows_u8", "rt_quantize_u8",
-               "rt_p3_row_lengths", "rt_format_p3_rows", "rt_strerror"]
+               "rt_strerror"]
 
 
 def host_lib() -> C.CDLL:
@@ -122,8 +122,6 @@ def host_lib() -> C.CDLL:
         if hasattr(L, "rth_write_ppm_u8"):   # absent from round-1..4 libraries (A/B baselines)
             L.rth_write_ppm_u8.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
             L.rth_ppm_write_rows_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-        if hasattr(L, "rth_ppm_write_text"):       # absent from round-1..5 libraries (A/B baselines)
-            L.rth_ppm_write_text.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_int]
         if hasattr(L, "rth_row_set"):     # absent from round-1 libraries (A/B baselines)
             L.rth_row_set.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)] * 4
         _host = L
@@ -178,10 +176,6 @@ def hip_lib() -> C.CDLL:
                                                   C.c_void_p, C.c_void_p]
         if hasattr(L, "rt_quantize_u8"):           # absent from round-1..3 libraries (A/B baselines)
             L.rt_quantize_u8.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
-        if hasattr(L, "rt_format_p3_rows"):        # absent from round-1..5 libraries (A/B baselines)
-            L.rt_p3_row_lengths.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
-            L.rt_format_p3_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                            C.c_void_p]
         L.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_longlong]
         L.rt_strerror.argtypes = [C.c_int]
         L.rt_strerror.restype = C.c_char_p
@@ -288,24 +282,6 @@ def deinterleave_rows_device(gathered_ptr: int, world: int, rows_per: int, W: in
     f = L.rt_deinterleave_rows_u8 if u8 else L.rt_deinterleave_rows
     _check(f(C.c_void_p(gathered_ptr), world, rows_per, W, H, block, C.c_void_p(image_ptr), C.c_void_p(stream)),
            "rt_deinterleave_rows")
-
-
-def p3_text_device(values, W: int, H: int, torch, stream: int = 0) -> bytes:
-    """The P3 writer's pixel text (main.cpp:628-648, without the header)
-    formatted on the device by rt_p3_row_lengths + rt_format_p3_rows from a
-    torch CUDA tensor of W*H*3 float32 (the image) or uint8 (the writer's
-    bytes); returned as host bytes."""
-    L = hip_lib()
-    kind = 1 if values.dtype == torch.uint8 else 0
-    row_len = torch.empty(H, dtype=torch.int64, device=values.device)
-    _check(L.rt_p3_row_lengths(C.c_void_p(values.data_ptr()), kind, W, H, C.c_void_p(row_len.data_ptr()),
-                               C.c_void_p(stream)), "rt_p3_row_lengths")
-    off = torch.cumsum(row_len, 0) - row_len
-    total = int(row_len.sum().item())
-    text = torch.empty(max(1, total), dtype=torch.uint8, device=values.device)
-    _check(L.rt_format_p3_rows(C.c_void_p(values.data_ptr()), kind, W, H, C.c_void_p(off.data_ptr()),
-                               C.c_void_p(text.data_ptr()), C.c_void_p(stream)), "rt_format_p3_rows")
-    return bytes(text[:total].cpu().numpy())
 
 
 def write_ppm(path: str, rgb: np.ndarray, threads: int = 0) -> None:

@@ -1288,25 +1288,21 @@ def test_device_init_repeated():
 
 @pytest.mark.parametrize("block", ["100000", "1", "7", "64"])
 def test_cli_streamed_ppm_matches(block, tmp_path):
-    """Without --float-out the one-device CLI formats the P3 text on the
-    device (write_ppm_device: rt_p3_row_lengths + rt_format_p3_rows, round
-    6) and copies it to the host in one piece, or -- 512 MB and more, or
-    whenever RT_PPM_TEXT_CHUNK is set -- in pieces through pinned buffers,
-    each written while the next copies.  RT_PPM_HOST selects the host
-    formatting paths: the writer's bytes quantised on the device and
-    formatted by the host writer in row blocks (write_ppm_bytes), falling back
-    to the floats when some value is not 0..255 (test7: NaN pixels), copied
-    in row blocks through pinned buffers (stream_ppm; RT_PPM_FLOATS forces
-    them).  Every way writes the P3 file byte for byte as the one written
-    from the whole float image (--float-out takes that path), for one block
-    and for 1-, 7- and 64-row blocks / byte pieces on ragged images."""
+    """Without --float-out the one-device CLI quantises the image on the
+    device and copies 3 bytes per pixel to the host in row blocks, each block
+    formatted as soon as it lands (write_ppm_bytes, rth_ppm_write_rows_u8);
+    when some value is not 0..255 (test7: NaN pixels) it falls back to the
+    floats, copied in row blocks through pinned buffers and written while the
+    next block copies (stream_ppm; images of 512 MB and more, or whenever
+    RT_PPM_BLOCK_ROWS is set; RT_PPM_FLOATS forces the floats).  Every way
+    writes the P3 file byte for byte as the one written from the whole float
+    image (--float-out takes that path), for one block and for 1-, 7- and
+    64-row blocks on ragged images."""
     import json as _json
     for name, want_from in (("test7_s.txt", "floats"), ("C3_64x64.txt", "bytes")):
         outs, froms = [], []
-        modes = [(["--float-out", str(tmp_path / "f.bin")], {}),
-                 ([], {"RT_PPM_HOST": "1", "RT_PPM_BLOCK_ROWS": block}),
-                 ([], {"RT_PPM_HOST": "1", "RT_PPM_BLOCK_ROWS": block, "RT_PPM_FLOATS": "1"}),
-                 ([], {}), ([], {"RT_PPM_TEXT_CHUNK": str(int(block) * 97 + 1)})]
+        modes = [(["--float-out", str(tmp_path / "f.bin")], {}), ([], {"RT_PPM_BLOCK_ROWS": block}),
+                 ([], {"RT_PPM_BLOCK_ROWS": block, "RT_PPM_FLOATS": "1"}), ([], {})]
         for args, env in modes:
             tmp_name = "_stream_" + name
             shutil.copy(os.path.join(SCENES, name), os.path.join(SCENES, tmp_name))
@@ -1323,7 +1319,7 @@ def test_cli_streamed_ppm_matches(block, tmp_path):
                     if os.path.exists(p):
                         os.remove(p)
         assert len(outs[0]) > 1000 and all(o == outs[0] for o in outs), (name, [len(o) for o in outs])
-        assert froms == ["floats", want_from, "floats", "device text", "device text"], (name, froms)
+        assert froms == ["floats", want_from, "floats", want_from], (name, froms)
 
 
 @pytest.mark.parametrize("name", ["test7_s.txt", "C3_64x64.txt"])
@@ -1380,7 +1376,7 @@ def test_cli_rccl_byte_gather_matches_host(name, want_from, tmp_path):
                 if os.path.exists(p):
                     os.remove(p)
     assert len(outs["host"]) > 100 and outs["host"] == outs["rccl"]
-    assert froms["host"] == "device text", froms         # one device: formatted on it
+    assert froms["rccl"] == froms["host"], froms
     if want_from:
         assert froms["rccl"] == want_from, froms
 
@@ -1417,39 +1413,6 @@ def test_cli_rccl_gather_multi_device(tmp_path):
                     os.remove(p)
     assert outs["host"][0] == outs["rccl"][0] == outs["rccl8"][0]
     assert np.array_equal(np.nan_to_num(outs["host"][1], nan=-9), np.nan_to_num(outs["rccl"][1], nan=-9))
-
-
-@pytest.mark.parametrize("W,H", [(1, 1), (7, 3), (256, 2), (257, 5), (1000, 9), (4099, 1)])
-def test_p3_text_device_matches_host_writer(W, H, tmp_path):
-    """rt_p3_row_lengths + rt_format_p3_rows (the reference's P3 text,
-    main.cpp:628-648, formatted on the device) give byte for byte the pixel
-    text of rth_write_ppm, for floats of every kind the writer formats -- the
-    0..255 table, NaN and +-inf (INT_MIN as size_t), above 1, negative,
-    beyond the int range -- and for the writer's bytes (rt_quantize_u8),
-    across row widths below, at and above the formatter's 256-pixel chunk."""
-    torch = pytest.importorskip("torch")
-    rng = np.random.default_rng(W * 31 + H)
-    n = W * H * 3
-    v = rng.random(n, dtype=np.float32)
-    special = np.array([np.nan, np.inf, -np.inf, 1.5, 255.0, -0.25, -1 / 255, 1e10, -1e10, 0.0, -0.0, 1.0,
-                        254.999 / 255, 8421504.0, 2147483520.0 / 255], dtype=np.float32)
-    k = rng.integers(0, n, size=min(n, 40))
-    v[k] = special[rng.integers(0, len(special), size=len(k))]
-    img = v.reshape(H, W, 3)
-    ref = str(tmp_path / "host.ppm")
-    rtamd.write_ppm(ref, img)
-    host = open(ref, "rb").read()
-    head = b"P3 \n%d %d \n255 \n" % (W, H)
-    assert host.startswith(head)
-    d = torch.from_numpy(img).to("cuda:0")
-    got = rtamd.p3_text_device(d, W, H, torch)
-    assert got == host[len(head):]
-    # the writer's bytes (values 0..255 only)
-    q8 = np.clip(rtamd.quantize(np.nan_to_num(np.clip(img, 0, 1))), 0, 255).astype(np.uint8)
-    ref8 = str(tmp_path / "host8.ppm")
-    rtamd.write_ppm_u8(ref8, q8)
-    got8 = rtamd.p3_text_device(torch.from_numpy(q8).to("cuda:0"), W, H, torch)
-    assert got8 == open(ref8, "rb").read()[len(head):]
 
 
 def test_quantize_u8_device():

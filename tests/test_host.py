@@ -156,39 +156,6 @@ def test_writer_in_row_blocks_matches():
         assert L.rth_ppm_close(h) == -1                                # 10 of 67 rows
 
 
-def test_writer_preformatted_text_matches():
-    """rth_ppm_write_text (the CLI's path for text formatted on the device,
-    rt_format_p3_rows) appends already-formatted pixel text: the file equals
-    write_ppm's byte for byte for any split of the text into pieces and any
-    thread count (pieces of >= 4 MB pwritten at once); rows not all counted
-    at close fail."""
-    rng = np.random.default_rng(11)
-    img = rng.uniform(-0.5, 1.5, size=(301, 517, 3)).astype(np.float32)
-    img[3, 4, 0] = np.nan
-    ref = ppm_bytes(img)
-    head = b"P3 \n517 301 \n255 \n"
-    assert ref.startswith(head)
-    text = ref[len(head):]
-    import tempfile
-    L = rtamd.host_lib()
-    with tempfile.TemporaryDirectory() as td:
-        p = os.path.join(td, "x.ppm")
-        for cuts, threads in (([], 1), ([1, 17, 4099], 3), ([len(text) // 2], 16), ([0, 0, 5], 8)):
-            h = C.c_void_p()
-            assert L.rth_ppm_open(os.fsencode(p), 517, 301, threads, C.byref(h)) == 0
-            edges = [0] + sorted(cuts) + [len(text)]
-            for k in range(len(edges) - 1):
-                piece = text[edges[k]:edges[k + 1]]
-                rows = 301 if k == len(edges) - 2 else 0
-                assert L.rth_ppm_write_text(h, piece, len(piece), rows) == 0
-            assert L.rth_ppm_close(h) == 0
-            assert open(p, "rb").read() == ref, (cuts, threads)
-        h = C.c_void_p()
-        assert L.rth_ppm_open(os.fsencode(p), 517, 301, 2, C.byref(h)) == 0
-        assert L.rth_ppm_write_text(h, text, len(text), 300) == 0
-        assert L.rth_ppm_close(h) == -1                                # 300 of 301 rows
-
-
 def test_output_path_is_remove_extension():
     assert rtamd.output_path("a/b/scene.txt") == "a/b/scene.ppm"
     assert rtamd.output_path("scene") == "scene.ppm"

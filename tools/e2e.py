@@ -30,19 +30,11 @@ def main():
     # --floats: the P3 file from the float image (RT_PPM_FLOATS), for an A/B
     # against the default byte path (device-quantised, 3 B per pixel)
     floats = "--floats" in sys.argv
-    # --host: the host formatting paths (RT_PPM_HOST) instead of the P3 text
-    # formatted on the device (round 6's default), for an A/B
-    host = "--host" in sys.argv
-    # --warm: one unrecorded run first (a fresh box's first HIP process pays
-    # for its first allocations and copies: 100-200 ms more)
-    warm = "--warm" in sys.argv
-    tag = ("_floats" if floats else "") + ("_host" if host else "")
-    env_x = {**({"RT_PPM_FLOATS": "1", "RT_PPM_HOST": "1"} if floats else {}), **({"RT_PPM_HOST": "1"} if host else {})}
+    tag = "_floats" if floats else ""
     cli = os.path.join(ROOT, "simple-raytracer_amd", "lib", "rt")
     od = os.path.join(ROOT, "gpurun_out")
     os.makedirs(od, exist_ok=True)
-    cfgs = args or ["C3", "C4", "C5"]
-    for k, cfg in enumerate(([cfgs[0]] if warm else []) + cfgs):
+    for cfg in args or ["C3", "C4", "C5"]:
         d = tempfile.mkdtemp(prefix=f"rte2e_{cfg}_")
         path = gen.write_scene(d, cfg)
         js = os.path.join(d, "stats.json")
@@ -51,7 +43,7 @@ def main():
         # RT_TIMING: the library's own step times (scene creation, BVH upload,
         # first launch) on stderr, kept in the record
         r = subprocess.run(cmd, cwd=d, capture_output=True, text=True, timeout=600,
-                           env={**os.environ, "RT_TIMING": "1", **env_x})
+                           env={**os.environ, "RT_TIMING": "1", **({"RT_PPM_FLOATS": "1"} if floats else {})})
         wall = time.perf_counter() - t0
         if r.returncode != 0:
             print(f"{cfg}: rt failed rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}", flush=True)
@@ -65,8 +57,6 @@ def main():
         ppm = os.path.splitext(path)[0] + ".ppm"
         if not keep and os.path.exists(ppm):
             os.remove(ppm)
-        if warm and k == 0:
-            continue                          # the unrecorded warm-up run
         with open(os.path.join(od, f"e2e_{cfg}{tag}.json"), "w") as f:
             json.dump(j, f, indent=1)
         print(json.dumps(j), flush=True)

@@ -55,7 +55,7 @@ for step in "$@"; do
       unset RTAMD_LIB_DIR ;;
     e2e)
       # a: extra flags (floats: the float writer, RT_PPM_FLOATS)
-      timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 --warm ${a:+--$a} > "$out/e2e$a.txt" 2>&1 || { tail -20 "$out/e2e$a.txt"; exit 1; } ;;
+      timeout -k 10 600 python -u tools/e2e.py C3 C4 C5 ${a:+--$a} > "$out/e2e$a.txt" 2>&1 || { tail -20 "$out/e2e$a.txt"; exit 1; } ;;
     phases)
       # RT_PROF build (make VARIANT=prof EXTRA=-DRT_PROF=1); b: extra options (counters=0)
       RTAMD_LIB_DIR=$GRAFT_REPO_ROOT/simple-raytracer_amd/lib_prof timeout -k 10 300 python -u tools/prof_phases.py \
