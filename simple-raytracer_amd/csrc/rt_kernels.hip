@@ -1650,6 +1650,10 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
     cnt.trips = 0;
     cnt.trips_kind[0] = cnt.trips_kind[1] = cnt.trips_kind[2] = 0;
     unsigned long long pc_shade = 0, pc_trace = 0, pc_bf = 0, pc_iter = 0, pc_lanes = 0, pc_wtrips = 0;
+    // lanes that sit a trace step out, by reason: no pixel (waiting for a
+    // refill batch, or the work has run out), a held reflection / refraction
+    // search, a known shadow result
+    unsigned long long pc_nopix = 0, pc_held = 0, pc_known = 0;
     unsigned long long pc_mixed = 0;     // trace steps with primary and secondary/shadow searches together
     unsigned long long t_drain = 0;
     unsigned long long n_refill = 0, pc_refill = 0;
@@ -1852,6 +1856,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
             pc_shade += c1 - c0;
             pc_iter++;
             pc_lanes += (unsigned long long)__popcll(__ballot(search && !q.bf));
+            pc_nopix += (unsigned long long)__popcll(__ballot(!pending));
+            pc_held += (unsigned long long)__popcll(__ballot(pending && held));
+            pc_known += (unsigned long long)__popcll(__ballot(pending && known));
             unsigned tr0 = cnt.trips;
 #endif
             // origin-leaf pass by the query's kind (held_kind: this step's):
@@ -1934,6 +1941,9 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
         atomicAdd(&st[11], pc_bf);
         atomicAdd(&st[12], pc_iter);
         atomicAdd(&st[13], pc_lanes);
+        atomicAdd(&st[50], pc_nopix);
+        atomicAdd(&st[51], pc_held);
+        atomicAdd(&st[52], pc_known);
         atomicAdd(&st[14], pc_wtrips);
         atomicAdd(&st[39], pc_mixed);
         atomicAdd(&st[46], pc_refill);               // cycles waiting for the work counter

@@ -66,6 +66,9 @@ def main():
         "work_counter_wait_cycles_per_refill": c[46] / c[47] if c[47] else None,
         "outer_iterations": iters,
         "trace_lane_occupancy": lanes / (64 * iters) if iters else None,
+        # the lanes that sit a step out, by reason (fractions of 64 x steps)
+        "idle_lanes_by_reason": {"no_pixel": c[50] / (64 * iters), "held_secondary": c[51] / (64 * iters),
+                                 "known_shadow": c[52] / (64 * iters)} if iters and len(c) > 52 else None,
         "traversal_simd_eff": ltrips / (64 * wtrips) if wtrips else None,
         "lane_trips_per_trace_lane": ltrips / lanes if lanes else None,
         "wave_trips_per_iter": wtrips / iters if iters else None,
