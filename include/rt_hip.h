@@ -142,7 +142,8 @@ int rt_device_count(void);
  * (a stream the next rt_scene_create on the device takes), the kernels' code
  * object -- ahead of rt_scene_create, e.g. on a thread while the scene file
  * is parsed (the CLI does: ~40-50 ms that would otherwise land in the first
- * scene upload and the first stats read).  Thread-safe; may be called again. */
+ * scene upload and the first stats read).  Thread-safe; may be called again:
+ * at most one such stream waits per device (a repeated call adds none). */
 int rt_device_init(int device);
 
 /* Upload a scene to HIP device `device`. */
