@@ -197,6 +197,12 @@ constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
 constexpr int kHeadStack = 3;            // medium-stack entries in a dense head slot
+#ifndef RT_HEAD_INTS
+#define RT_HEAD_INTS 8                   // 4-B words per dense head slot (acc, f, meta, kHeadStack entries;
+                                         // 16: a probe of what the slots' density buys)
+#endif
+constexpr int kHeadInts = RT_HEAD_INTS;
+static_assert(kHeadInts >= 5 + kHeadStack, "head slot");
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

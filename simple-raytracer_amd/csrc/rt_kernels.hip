@@ -1274,7 +1274,7 @@ struct LaneState {
         unsigned t;
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         // (slot index < 2^25: levels <= 17, lanes of the grid < 2^20)
-        f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * 8;
+        f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * kHeadInts;
         }
         return f;
     }

@@ -256,7 +256,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     // recursive instantiations (dense_heads): the frame heads, [block][level]
     // [lane] 32-B slots, after the spill area (Params::heads, LaneState::fr)
     const size_t heads_off = (fbytes + 255) / 256 * 256;
-    if (dense_heads(maxf)) fbytes = heads_off + (size_t)grid * kBlock * maxf * 32;
+    if (dense_heads(maxf)) fbytes = heads_off + (size_t)grid * kBlock * maxf * kHeadInts * 4;
     if (slot.frames_cap < fbytes) {
         // (re)size every slot's buffer now, not each at its first use: a
         // frame pipeline then allocates once, in its first (warm-up) frame
