@@ -196,13 +196,22 @@ constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 #endif
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
-constexpr int kHeadStack = 3;            // medium-stack entries in a dense head slot
+#ifndef RT_HEAD_SPLIT
+#define RT_HEAD_SPLIT 0                  // 1: a dense slot's 32 B as two 16-B slots in two arrays -- acc, f in one,
+                                         // the child's first 4 stack entries in the other (rt_kernels.hip Fr)
+#endif
+constexpr bool kHeadSplit = RT_HEAD_SPLIT;
+// split for MAXF <= 9 (the node's meta then carries a bit per level, rt_kernels.hip kKindsShift)
+constexpr bool head_split(int maxf) { return kHeadSplit && dense_heads(maxf) && maxf <= 9; }
+constexpr int kSplitLightBits = 15;      // light index bits of a head_split instantiation's meta
+constexpr int kSplitLightMax = (1 << kSplitLightBits) - 1;   // more lights: MAXF 17 (rt_scene.cpp)
+constexpr int head_stack(int maxf) { return head_split(maxf) ? 4 : 3; }   // medium-stack entries in a dense slot
 #ifndef RT_HEAD_INTS
 #define RT_HEAD_INTS 8                   // 4-B words per dense head slot (acc, f, meta, kHeadStack entries;
                                          // 16: a probe of what the slots' density buys)
 #endif
 constexpr int kHeadInts = RT_HEAD_INTS;
-static_assert(kHeadInts >= 5 + kHeadStack, "head slot");
+static_assert(kHeadInts >= 5 + 3 && (!kHeadSplit || kHeadInts == 8), "head slot");
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

@@ -776,7 +776,17 @@ struct HotR {                        // register form of the top node's state
 __device__ __forceinline__ int h_phase(const HotR &h) { return (int)(h.meta & 7u); }
 __device__ __forceinline__ int h_state(const HotR &h) { return (int)((h.meta >> 3) & 1u); }
 __device__ __forceinline__ int h_sn(const HotR &h) { return (int)((h.meta >> 4) & 31u); }
-__device__ __forceinline__ int h_light(const HotR &h) { return (int)(h.meta >> 9); }
+// The split head slots (head_split) keep no meta: their instantiations keep in
+// the top byte of a node's meta a bit per level above it -- bit kKindsShift + k:
+// the node at level k + 1 on its path is a refraction child -- and the light
+// index in the 15 bits below (scenes of more lights take MAXF 17, rt_scene.cpp)
+constexpr int kKindsShift = 24;
+constexpr unsigned kKindsMask = 0xFF000000u;
+static_assert(kKindsShift - 9 == kSplitLightBits, "meta: light bits below the kinds");
+template <int MAXF>
+__device__ __forceinline__ int h_light(const HotR &h) {
+    return head_split(MAXF) ? (int)((h.meta >> 9) & ((1u << kSplitLightBits) - 1)) : (int)(h.meta >> 9);
+}
 __device__ __forceinline__ unsigned mk_meta(int phase, int state, int sn, int light) {
     return (unsigned)phase | ((unsigned)state << 3) | ((unsigned)sn << 4) | ((unsigned)light << 9);
 }
@@ -821,7 +831,11 @@ __device__ __forceinline__ LightW light_words(const Params &p, int i) {
 }
 
 __device__ __forceinline__ float *lane_lds() { return reinterpret_cast<float *>(rt_lds) + threadIdx.x; }
-__device__ __forceinline__ int h_light_lds() { return (int)(__float_as_uint(lane_lds()[LW_META * kBlock]) >> 9); }
+template <int MAXF>
+__device__ __forceinline__ int h_light_lds() {
+    const unsigned meta = __float_as_uint(lane_lds()[LW_META * kBlock]);
+    return head_split(MAXF) ? (int)((meta >> 9) & ((1u << kSplitLightBits) - 1)) : (int)(meta >> 9);
+}
 __device__ __forceinline__ void lds_load(HotR &h) {
     const float *l = lane_lds();
     h.N = {l[(LW_N + 0) * kBlock], l[(LW_N + 1) * kBlock], l[(LW_N + 2) * kBlock]};
@@ -878,7 +892,8 @@ struct Cold {
     int stack[MAXF];                 // the CHILD's medium stack (incident_object_stack), object indices
     int pad0_[(cold_ext(MAXF) - 20 - 4 * MAXF) / 4];
     float4 ext[3];                   // (N, I.x), (I.y, I.z, obj, eta_i), (eta_t, P)
-    int pad1_[(cold_size(MAXF) - cold_ext(MAXF) - 48) / 4];
+    unsigned xmeta;                  // kHeadSplit: the node's meta (its head slot has no room for it)
+    int pad1_[(cold_size(MAXF) - cold_ext(MAXF) - 52) / 4];
 };
 static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17>) == 192, "cold frame sizes");
 static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's frame is one 64-B half line");
@@ -910,10 +925,11 @@ struct Fr<MAXF, true> {              // dense heads (dense_heads(MAXF))
     static constexpr bool kDense = true;
     Cold<MAXF> *c;
     int *hs;
-    __device__ __forceinline__ int stk(int i) const { return i < kHeadStack ? hs[5 + i] : c->stack[i]; }
+    int *ss;                         // kHeadSplit: the stack slot (else hs + 5)
+    __device__ __forceinline__ int stk(int i) const { return i < head_stack(MAXF) ? ss[i] : c->stack[i]; }
     __device__ __forceinline__ void set_stk(int i, int v) const {
-        if (i < kHeadStack)
-            hs[5 + i] = v;
+        if (i < head_stack(MAXF))
+            ss[i] = v;
         else
             c->stack[i] = v;
     }
@@ -922,7 +938,7 @@ template <int MAXF>
 __device__ __forceinline__ void cold_save_head(const Fr<MAXF> &fr, const HotR &h, float f) {
     if constexpr (Fr<MAXF>::kDense) {
         reinterpret_cast<f4v *>(fr.hs)[0] = f4v{h.acc.r, h.acc.g, h.acc.b, f};
-        fr.hs[4] = (int)h.meta;
+        if constexpr (!head_split(MAXF)) fr.hs[4] = (int)h.meta;
     } else {
         Cold<MAXF> &c = *fr.c;
         reinterpret_cast<f4v &>(c.head) = f4v{h.acc.r, h.acc.g, h.acc.b, f};
@@ -935,6 +951,7 @@ __device__ __forceinline__ void cold_save_ext(const Fr<MAXF> &fr, V3 P, const Ho
     v[0] = f4v{h.N.x, h.N.y, h.N.z, h.I.x};
     v[1] = f4v{h.I.y, h.I.z, __int_as_float(h.obj), h.ei};
     v[2] = f4v{h.et, P.x, P.y, P.z};
+    if constexpr (head_split(MAXF)) fr.c->xmeta = h.meta;
 }
 // the head: h.acc, h.meta; returns f
 template <int MAXF>
@@ -942,7 +959,7 @@ __device__ __forceinline__ float cold_restore_head(const Fr<MAXF> &fr, HotR &h) 
     f4v a;
     if constexpr (Fr<MAXF>::kDense) {
         a = reinterpret_cast<const f4v *>(fr.hs)[0];
-        h.meta = (unsigned)fr.hs[4];
+        if constexpr (!head_split(MAXF)) h.meta = (unsigned)fr.hs[4];
     } else {
         a = reinterpret_cast<const f4v &>(fr.c->head);
         h.meta = fr.c->meta;
@@ -960,6 +977,7 @@ __device__ __forceinline__ V3 cold_restore_ext(const Fr<MAXF> &fr, HotR &h) {
     h.obj = __float_as_int(b.z);
     h.ei = b.w;
     h.et = d.x;
+    if constexpr (head_split(MAXF)) h.meta = fr.c->xmeta;
     return V3{d.y, d.z, d.w};
 }
 
@@ -1087,6 +1105,7 @@ __device__ __forceinline__ void copy_stack(const HotR &f, const Fr<MAXF> &fc, co
 struct Medium {
     int state, sn;
     float ei, et;
+    unsigned kinds;                  // head_split: the child's meta kinds (kKindsShift)
 };
 
 __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m) {
@@ -1130,7 +1149,7 @@ __device__ V3 node_open(const Params &p, int obj, V3 o, V3 d, float t, Medium m)
     h.dif = dif;
     h.acc = C3{0.0f, 0.0f, 0.0f};    // tmp_specular while lights run
     h.obj = obj;
-    h.meta = mk_meta(PH_LIGHT, m.state, m.sn, 0);
+    h.meta = mk_meta(PH_LIGHT, m.state, m.sn, 0) | m.kinds;
     h.ei = m.ei;
     h.et = m.et;
     lds_store(h);
@@ -1274,7 +1293,14 @@ struct LaneState {
         unsigned t;
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         // (slot index < 2^25: levels <= 17, lanes of the grid < 2^20)
-        f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * kHeadInts;
+        if constexpr (head_split(MAXF)) {
+            const size_t slot = (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t);
+            f.hs = static_cast<int *>(p.heads) + slot * 4;
+            f.ss = static_cast<int *>(p.heads) + ((size_t)gridDim.x * MAXF * kBlock + slot) * 4;
+        } else {
+            f.hs = static_cast<int *>(p.heads) + (size_t)((blockIdx.x * MAXF + (unsigned)k) * kBlock + t) * kHeadInts;
+            f.ss = f.hs + 5;
+        }
         }
         return f;
     }
@@ -1349,7 +1375,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             color = bkg;
             return RK_NONE;
         }
-        m = Medium{ENTERING, 1, p.eta_bkg, row(p.objs, q.win).eta};   // stack {q.win}: implicit (copy_stack)
+        m = Medium{ENTERING, 1, p.eta_bkg, row(p.objs, q.win).eta, 0u};   // stack {q.win}: implicit (copy_stack)
         open = true;
         top = 0;
     } else {
@@ -1359,7 +1385,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             // one light step per iteration (the loop continues only past known
             // shadow rays, below)
             for (;;) {
-                const int light = h_light(h);
+                const int light = h_light<MAXF>(h);
                 const ObjK &ob = row(p.objs, h.obj);
                 // the light's words in one batch (LightK: xyz w | col | L)
                 const LightW lw = light_words(p, light);
@@ -1465,6 +1491,8 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
             // dif.r: F_t (refraction child) or F_r (reflection child)
             if (h_phase(h) == PH_REFR_CHILD) cold_save_ext(c, q.o, h);
             cold_save_head(c, h, h.dif.r);
+            if constexpr (head_split(MAXF))          // the child's kinds: ours and its own
+                m.kinds = (h.meta & kKindsMask) | ((unsigned)(h_phase(h) == PH_REFR_CHILD) << (kKindsShift + top));
             top++;
         }
     }
@@ -1538,7 +1566,7 @@ __device__ int advance(const Params &p, LaneState<MAXF> &ls, Query &q, CNT &cnt,
         top--;
         const Fr<MAXF> pc = ls.fr(p, top);
         const float f = cold_restore_head(pc, h);
-        if (h_phase(h) == PH_REFR_CHILD) {           // main.cpp:1072-1083
+        if (head_split(MAXF) ? ((h.meta >> (kKindsShift + top)) & 1u) != 0 : h_phase(h) == PH_REFR_CHILD) {   // main.cpp:1072-1083
             q.o = cold_restore_ext(pc, h);
             h.dif.r = f;                             // F_t
             const ObjK &pob = row(p.objs, h.obj);
@@ -1878,7 +1906,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                 const bool pt = search && !q.closest && q.unb && !q.bf &&
                                 !(p.shadow_early_out && q.mask == 0.0f);
                 if (__ballot(pt) && pt) {
-                    const DirK &dk = p.dirk[h_light_lds()];
+                    const DirK &dk = p.dirk[h_light_lds<MAXF>()];
                     const int root = dk.root;
                     if (root >= 0) {
                         V3 po = {fmaf(dk.R[0], q.o.x, fmaf(dk.R[1], q.o.y, dk.R[2] * q.o.z)),

@@ -374,8 +374,9 @@ int build_bvh(rt_scene *s, double D) {
 
 int launch(rt_scene *s, RenderSlot &slot, Params &p, hipStream_t st, bool dry = false) {
     int depth = p.depth < 0 ? 0 : p.depth;
-    const int maxf = maxf_for(depth, s->secondary || (s->opt_recursive && depth > 0));
+    int maxf = maxf_for(depth, s->secondary || (s->opt_recursive && depth > 0));
     if (maxf < 0) return RT_E_UNSUPPORTED;
+    if (head_split(maxf) && p.nl > kSplitLightMax) maxf = 17;   // its meta's light index field (rt_device.h)
     int nobj = p.nf + p.ns;
     bool bvh = s->opt_accel == 1 || (s->opt_accel == -1 && nobj > 32);
     int mode = MODE_SCAN;

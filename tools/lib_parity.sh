@@ -8,4 +8,4 @@ lib=$1; shift
 export RTAMD_LIB_DIR=${GRAFT_REPO_ROOT:-$(pwd)}/simple-raytracer_amd/$lib
 exec python -m pytest tests/test_gpu_parity.py tests/test_float_goldens.py -m gpu -q -p no:cacheprovider --maxfail=${MAXFAIL:-12} \
   --timeout 300 --timeout-method thread \
-  -k "golden or reference_floats or depth_knob or bit_identical or c3_full or c3_variants or lds_stack" "$@"
+  -k "${K:-golden or reference_floats or depth_knob or bit_identical or c3_full or c3_variants or lds_stack}" "$@"
