@@ -287,7 +287,9 @@ int rt_scene_set_option(rt_scene *scene, const char *key, long long value);
  * in LDS (1) or read from device memory (0), [44] 0 (on the device this slot
  * counts the ub_back events, which rt_scene_debug_ub_pixels returns; rounds
  * 4-5 reported the removed option hot_copies here), [45] work bands (option
- * work_parts), [48] the counting kernel instantiation (option counters: 1)
+ * work_parts), [46] frames per lane of the kernel instantiation (1, 5, 9 or
+ * 17: by depth; 17 also for depth <= 8 with more than 32767 lights), [47] its
+ * frame slots split (1: 16-B colour slots apart from the stack slots) or not, [48] the counting kernel instantiation (option counters: 1)
  * or the one without counters (0); RT_CHECK builds: [49] stack-bottom
  * invariant violations (must be 0).  n <= 64. */
 int rt_scene_debug_counters(rt_scene *scene, unsigned long long *out, int n);

@@ -197,8 +197,9 @@ constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
 #ifndef RT_HEAD_SPLIT
-#define RT_HEAD_SPLIT 0                  // 1: a dense slot's 32 B as two 16-B slots in two arrays -- acc, f in one,
-                                         // the child's first 4 stack entries in the other (rt_kernels.hip Fr)
+#define RT_HEAD_SPLIT 1                  // a dense slot's 32 B as two 16-B slots in two arrays -- acc, f in one,
+                                         // the child's first 4 stack entries in the other (rt_kernels.hip Fr);
+                                         // 0: one 32-B slot (acc, f, meta, 3 entries), rounds 5-6
 #endif
 constexpr bool kHeadSplit = RT_HEAD_SPLIT;
 // split for MAXF <= 9 (the node's meta then carries a bit per level, rt_kernels.hip kKindsShift)
@@ -219,7 +220,7 @@ constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.
 #endif
 constexpr int kOrgFirst = RT_ORG_FIRST;
 constexpr double kOrgDensity = 32.0;     // objects met by a line across the scene (C3 ~3, C5 ~200)
-constexpr int kNStats = 64;              // counter slots (rt_scene_debug_counters; the device writes 0..39, 44..47)
+constexpr int kNStats = 64;              // counter slots (rt_scene_debug_counters; the device writes 0..39, 44)
 // RT_PROF builds: a per-wave timeline after the counters (rt_scene_debug_wavelog),
 // kWaveLogWords words per wave: launch start, prologue done, work drained (0:
 // never saw it), end (100 MHz ticks), HW_ID, XCC_ID, outer iterations, refills

@@ -892,27 +892,38 @@ struct Cold {
     int stack[MAXF];                 // the CHILD's medium stack (incident_object_stack), object indices
     int pad0_[(cold_ext(MAXF) - 20 - 4 * MAXF) / 4];
     float4 ext[3];                   // (N, I.x), (I.y, I.z, obj, eta_i), (eta_t, P)
-    unsigned xmeta;                  // kHeadSplit: the node's meta (its head slot has no room for it)
+    unsigned xmeta;                  // head_split: the node's meta (its head slot keeps none)
     int pad1_[(cold_size(MAXF) - cold_ext(MAXF) - 52) / 4];
 };
 static_assert(sizeof(Cold<5>) == 128 && sizeof(Cold<9>) == 128 && sizeof(Cold<17>) == 192, "cold frame sizes");
 static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's frame is one 64-B half line");
 
 // One level's frame as the shading code sees it: the lane's Cold record and,
-// in the recursive instantiations (dense_heads(MAXF)), the level's 32-B head
-// slot in a dense head array -- acc, f, meta and the first kHeadStack
-// medium-stack entries; the slots of one level for consecutive lanes of a
-// workgroup are consecutive, so a wave's heads share lines.  Stack entries from kHeadStack
-// on, and a refraction child's extension, stay in the Cold record.
+// in the recursive instantiations (dense_heads(MAXF)), the level's slots in
+// dense arrays ([block][level][lane], from Params::heads): the slots of one
+// level for consecutive lanes of a workgroup are consecutive, so a wave's
+// slots share lines.  Stack entries past the dense ones, and a refraction
+// child's extension, stay in the Cold record.
+//  * head_split(MAXF) (MAXF 5 and 9): a 16-B head slot -- acc, f -- and, in a
+//    second array after the heads, a 16-B stack slot -- the child's first 4
+//    medium-stack entries.  The node's meta is not saved with the head: a
+//    reflection child's return needs only acc and f (the parent is then
+//    complete), a refraction child's return reads the extension anyway, and
+//    the meta travels there (Cold::xmeta); which of the two the parent
+//    opened is a bit of the child's own meta (kKindsShift).
+//  * MAXF 17 (or RT_HEAD_SPLIT=0): one 32-B slot -- acc, f, meta and the
+//    first 3 stack entries.
 //
 // Why: a child's return reads its parent's head back after the child's
 // whole subtree, and with each head alone in a 128-B line of a 377-MB frame
 // area (C5) that read missed L2 nearly every time -- the head stream was
-// ~140 of C5's 266 GB read (the head-copy probe).  Dense heads
-// ([block][level][lane], from Params::heads): C5 266 -> 166 GB read, +2.1 %;
-// C3 3.5 -> 2.0 GB read, +0.4 % (profiles/r05/ab/dense_heads_*).  (Addressed
-// [level][lane] over the whole grid instead, the slot arithmetic cost C3
-// 0.2 ... 0.7 %.)
+// ~140 of C5's 266 GB read (the head-copy probe).  Dense 32-B
+// slots: C5 266 -> 166 GB read, +2.1 %; C3 3.5 -> 2.0 GB read, +0.4 %
+// (profiles/r05/ab/dense_heads_*).  The returns' line misses follow the slot
+// density (64-B slots: C5 215 GB read, -1.7 %, profiles/r06/heads); the split
+// 16-B heads: C5 154 -> 104 GB read, +0.7 %; C3 +0.2 % (profiles/r06/heads/
+// ab_split_*).  (Addressed [level][lane] over the whole grid instead, the
+// slot arithmetic cost C3 0.2 ... 0.7 %.)
 template <int MAXF, bool D = dense_heads(MAXF)>
 struct Fr {                          // plain frames (and MAXF = 1, which opens no child)
     static constexpr bool kDense = false;
@@ -925,7 +936,7 @@ struct Fr<MAXF, true> {              // dense heads (dense_heads(MAXF))
     static constexpr bool kDense = true;
     Cold<MAXF> *c;
     int *hs;
-    int *ss;                         // kHeadSplit: the stack slot (else hs + 5)
+    int *ss;                         // the stack slot (head_split: its own array; else hs + 5)
     __device__ __forceinline__ int stk(int i) const { return i < head_stack(MAXF) ? ss[i] : c->stack[i]; }
     __device__ __forceinline__ void set_stk(int i, int v) const {
         if (i < head_stack(MAXF))
@@ -1282,10 +1293,11 @@ struct LaneState {
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((unsigned)threadIdx.x));
         return reinterpret_cast<Cold<MAXF> *>(frames) + ((size_t)blockIdx.x * kBlock + t) * MAXF;
     }
-    // level k's frame; the dense heads (dense_heads: Params::heads, after the
+    // level k's frame; the dense slots (dense_heads: Params::heads, after the
     // frames and the spill area, rt_scene.cpp launch_one) are [block][level]
-    // [lane] 32-B slots -- addressed where used, like the frames, rather than
-    // held in registers across the traversal
+    // [lane] -- 16-B heads then 16-B stack slots (head_split), or 32-B slots --
+    // addressed where used, like the frames, rather than held in registers
+    // across the traversal
     __device__ __forceinline__ Fr<MAXF> fr(const Params &p, int k) const {
         Fr<MAXF> f;
         f.c = cold() + k;

@@ -96,7 +96,7 @@ struct rt_scene {
     bool bvh_ok = false;
     double bvh_build_ms = 0.0;         // host time of the last BVH (re)build
     long long last_blocks_per_cu = 0, last_grid = 0, last_lds = 0, last_mode = -1;
-    long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0, last_work_parts = 0;
+    long long last_org_first = 0, last_stack_cap = 0, last_lights_in_lds = 0, last_work_parts = 0, last_maxf = 0;
     long long bvh_nodes = 0;
     bool last_valid = false;
 };
@@ -254,7 +254,8 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     const size_t cold_bytes = (size_t)grid * kBlock * maxf * cold_frame_bytes(maxf);
     size_t fbytes = cold_bytes + (size_t)grid * kBlock * s->ovf_stride * sizeof(int);
     // recursive instantiations (dense_heads): the frame heads, [block][level]
-    // [lane] 32-B slots, after the spill area (Params::heads, LaneState::fr)
+    // [lane] 32 B per slot (head_split: 16-B heads, then as many 16-B stack
+    // slots), after the spill area (Params::heads, LaneState::fr)
     const size_t heads_off = (fbytes + 255) / 256 * 256;
     if (dense_heads(maxf)) fbytes = heads_off + (size_t)grid * kBlock * maxf * kHeadInts * 4;
     if (slot.frames_cap < fbytes) {
@@ -281,6 +282,7 @@ hipError_t launch_one(rt_scene *s, RenderSlot &slot, const Params &p, int maxf, 
     s->last_stack_cap = pl.stack_cap;
     s->last_lights_in_lds = pl.lights_in_lds;
     s->last_work_parts = 1 << pl.work_shift;
+    s->last_maxf = maxf;
     if (dry) return hipSuccess;                  // rt_scene_prepare: buffers only
     const hipError_t e = render_launch(maxf, mode, s->opt_counters != 0, pl, (unsigned)grid, shm, st);
     tm.mark("kernel launch (enqueue)");
@@ -953,6 +955,8 @@ int rt_scene_debug_counters(rt_scene *s, unsigned long long *out, int n) {
     h[43] = (unsigned long long)s->last_lights_in_lds;
     h[45] = (unsigned long long)s->last_work_parts;
     h[44] = 0;                                   // (round 4-5: the BVH top copies, option removed)
+    h[46] = (unsigned long long)s->last_maxf;
+    h[47] = head_split((int)s->last_maxf) ? 1 : 0;
     h[48] = (unsigned long long)s->opt_counters;
     for (int i = 0; i < n; i++) out[i] = h[i];
     return RT_OK;

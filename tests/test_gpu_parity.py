@@ -770,6 +770,26 @@ def test_many_lights(accel, tmp_path):
     assert cnt["shadow"] >= 3000
 
 
+@pytest.mark.parametrize("n,maxf,split", [(32767, 5, 1), (32768, 17, 0)])
+def test_many_lights_meta_limit(n, maxf, split, tmp_path):
+    """The split frame slots' instantiations (MAXF 5 and 9) keep the light
+    index in 15 bits of a node's meta, the level kinds above it: 32767 lights
+    run there (the index reaches 32767 after the last light), 32768 take the
+    MAXF 17 instantiation, whose meta keeps 23 bits.  Both against the oracle,
+    with identical ray counts (glass and mirror spheres: refraction and
+    reflection children on every level)."""
+    (tmp_path / "many.txt").write_text(_many_lights_text(n))
+    hs = rtamd.HostScene("many.txt", cwd=str(tmp_path))
+    gs = rtamd.GpuScene(hs)
+    img, st = gs.render_rows(hs.camera(), hs.width, hs.height, 0, hs.height)
+    dbg = gs.debug_counters()
+    gs.close()
+    ref, cnt = OracleScene("many.txt", cwd=str(tmp_path)).render()
+    assert_parity(np.asarray(img).reshape(ref.shape), ref, f"{n} lights")
+    assert _counts(st) == cnt and cnt["refraction"] > 0 and cnt["reflection"] > 0
+    assert (dbg[46], dbg[47]) == (maxf, split)
+
+
 def _deep_scene_text(w: int = 32, h: int = 32) -> str:
     """Four arms of spheres at geometrically growing distance (1.08^k, k < 200)
     from the view axis and along it: a skewed tree (worst-case stack 27 with
