@@ -196,23 +196,15 @@ constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
 #endif
 constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
 constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
-#ifndef RT_HEAD_SPLIT
-#define RT_HEAD_SPLIT 1                  // a dense slot's 32 B as two 16-B slots in two arrays -- acc, f in one,
-                                         // the child's first 4 stack entries in the other (rt_kernels.hip Fr);
-                                         // 0: one 32-B slot (acc, f, meta, 3 entries), rounds 5-6
-#endif
-constexpr bool kHeadSplit = RT_HEAD_SPLIT;
-// split for MAXF <= 9 (the node's meta then carries a bit per level, rt_kernels.hip kKindsShift)
-constexpr bool head_split(int maxf) { return kHeadSplit && dense_heads(maxf) && maxf <= 9; }
+// The dense frame slots of an instantiation with MAXF <= 9 are split: 16-B
+// colour heads and 16-B stack slots in two arrays, the node's meta carrying a
+// bit per level instead (rt_kernels.hip Fr, kKindsShift); MAXF 17 keeps one
+// 32-B slot per level (acc, f, meta, 3 stack entries).  32 B per slot either way.
+constexpr bool head_split(int maxf) { return dense_heads(maxf) && maxf <= 9; }
 constexpr int kSplitLightBits = 15;      // light index bits of a head_split instantiation's meta
 constexpr int kSplitLightMax = (1 << kSplitLightBits) - 1;   // more lights: MAXF 17 (rt_scene.cpp)
 constexpr int head_stack(int maxf) { return head_split(maxf) ? 4 : 3; }   // medium-stack entries in a dense slot
-#ifndef RT_HEAD_INTS
-#define RT_HEAD_INTS 8                   // 4-B words per dense head slot (acc, f, meta, kHeadStack entries;
-                                         // 16: a probe of what the slots' density buys)
-#endif
-constexpr int kHeadInts = RT_HEAD_INTS;
-static_assert(kHeadInts >= 5 + 3 && (!kHeadSplit || kHeadInts == 8), "head slot");
+constexpr int kHeadInts = 8;             // 4-B words per dense slot (a 64-B slot: C5 -1.7 %, profiles/r06/heads)
 constexpr unsigned kGateX = 32;          // option gate_x (A/B: 24..48 within 0.2 % on C3 and C5)
 #ifndef RT_ORG_FIRST
 #define RT_ORG_FIRST 6                   // option org_first: origin-leaf pass for shadow (1) / refraction (2) /

@@ -911,7 +911,7 @@ static_assert(cold_ext(5) == 64 && cold_ext(9) == 64, "a reflection child's fram
 //    complete), a refraction child's return reads the extension anyway, and
 //    the meta travels there (Cold::xmeta); which of the two the parent
 //    opened is a bit of the child's own meta (kKindsShift).
-//  * MAXF 17 (or RT_HEAD_SPLIT=0): one 32-B slot -- acc, f, meta and the
+//  * MAXF 17: one 32-B slot -- acc, f, meta and the
 //    first 3 stack entries.
 //
 // Why: a child's return reads its parent's head back after the child's
