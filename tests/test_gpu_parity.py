@@ -1508,3 +1508,85 @@ def test_bvh_upload_failure_leaves_no_stale_tree():
     b, sb = gs.render_rows(cam, W, H, 0, H)
     assert np.array_equal(np.nan_to_num(a, nan=-9), np.nan_to_num(b, nan=-9))
     assert gs.debug_counters()[16] == 2           # BVH mode again
+
+
+def _random_scene_text(seed: int) -> tuple[str, int]:
+    """A seeded random scene for the state machine's corners: nested and
+    overlapping transparent spheres (deep medium stacks, exits without an
+    entry), glass and mirror materials, eta 1 (F0 = 0), opaque and zero-ks
+    objects, faces with and without vertex normals, point and directional
+    lights, a background brighter than 1 or negative, an eye inside a glass
+    sphere (refraction exits with an empty medium stack: ub_back), up to ~120
+    spheres (the BVH by default), and a depth from 1 to 10
+    -- the MAXF 5, 9 and 17 instantiations.  Returns (text, depth)."""
+    import random
+    r = random.Random(1000 + seed)
+    W, H = r.randint(6, 22), r.randint(5, 18)
+    bk = [r.choice([0.1, 0.3, 0.7, 1.4, -0.2]) for _ in range(3)]
+    bkg = f"bkgcolor {bk[0]} {bk[1]} {bk[2]}" + (f" {r.choice([1, 1.33])}" if r.random() < 0.7 else "")
+    out = [f"eye {r.uniform(-0.5, 0.5):.3f} {r.uniform(-0.5, 0.5):.3f} 0\nviewdir {r.uniform(-0.2, 0.2):.3f} "
+           f"{r.uniform(-0.2, 0.2):.3f} -1\nupdir 0 1 0\nhfov {r.randint(35, 80)}\nimsize {W} {H}\n{bkg}\n"]
+    for _ in range(r.randint(1, 4)):
+        w = 1 if r.random() < 0.7 else 0
+        p = (r.uniform(-8, 8), r.uniform(-2, 9), r.uniform(-9, 3)) if w else (r.uniform(-1, 1), r.uniform(-1, 0.2),
+                                                                                r.uniform(-1, 0.3))
+        c = [r.uniform(0.1, 1) for _ in range(3)]
+        out.append(f"light {p[0]:.3f} {p[1]:.3f} {p[2]:.3f} {w} {c[0]:.3f} {c[1]:.3f} {c[2]:.3f}\n")
+
+    def mtl():
+        od = [r.uniform(0, 1) for _ in range(3)]
+        os_ = [r.uniform(0.5, 1) for _ in range(3)]
+        ks = r.choice([0.0, 0.2, 0.5, 0.9])
+        base = (f"mtlcolor {od[0]:.3f} {od[1]:.3f} {od[2]:.3f} {os_[0]:.2f} {os_[1]:.2f} {os_[2]:.2f} "
+                f"{r.uniform(0.05, 0.3):.2f} {r.uniform(0.2, 0.8):.2f} {ks} {r.choice([2, 10, 40])}")
+        kind = r.random()
+        if kind < 0.35:
+            return base + "\n"                                   # opaque, no eta
+        op = r.choice([0.1, 0.3, 0.6, 0.9, 1.0])
+        eta = r.choice([1.0, 1.33, 1.5, 2.4])
+        return base + f" {op} {eta}\n"
+
+    if r.random() < 0.15:                                        # the eye inside a glass sphere
+        out.append(f"mtlcolor 0.9 0.9 0.9 1 1 1 0.1 0.3 0.5 20 {r.choice([0.2, 0.7])} {r.choice([1.2, 1.5])}\n")
+        out.append("sphere 0 0 0 25\n")
+    for _ in range(r.randint(2, 14) if r.random() < 0.8 else r.randint(30, 60)):   # spheres, some nested
+        out.append(mtl())
+        cx, cy, cz, rad = r.uniform(-3, 3), r.uniform(-2, 2), r.uniform(-12, -3), r.uniform(0.3, 1.6)
+        out.append(f"sphere {cx:.3f} {cy:.3f} {cz:.3f} {rad:.3f}\n")
+        if r.random() < 0.35:                                    # a concentric inner sphere
+            out.append(mtl())
+            out.append(f"sphere {cx:.3f} {cy:.3f} {cz:.3f} {rad * r.uniform(0.3, 0.8):.3f}\n")
+    nv = 0
+    for _ in range(r.randint(0, 10)):                            # triangles
+        out.append(mtl())
+        c = (r.uniform(-3, 3), r.uniform(-2, 2), r.uniform(-12, -3))
+        for _ in range(3):
+            out.append(f"v {c[0] + r.uniform(-2, 2):.3f} {c[1] + r.uniform(-2, 2):.3f} {c[2] + r.uniform(-1.5, 1.5):.3f}\n")
+        if r.random() < 0.4:
+            out.append(f"vn {r.uniform(-1, 1):.3f} {r.uniform(-1, 1):.3f} {r.uniform(0.2, 1):.3f}\n"
+                       f"vn {r.uniform(-1, 1):.3f} {r.uniform(-1, 1):.3f} {r.uniform(0.2, 1):.3f}\n"
+                       f"vn {r.uniform(-1, 1):.3f} {r.uniform(-1, 1):.3f} {r.uniform(0.2, 1):.3f}\n")
+            out.append(f"f {nv + 1}//{nv + 1} {nv + 2}//{nv + 2} {nv + 3}//{nv + 3}\n")
+        else:
+            out.append(f"f {nv + 1} {nv + 2} {nv + 3}\n")
+        nv += 3
+    return "".join(out), r.randint(1, 10)
+
+
+@pytest.mark.parametrize("seed", range(256))
+def test_random_scenes_parity(seed, tmp_path):
+    """256 seeded random scenes (`_random_scene_text`) against the oracle on
+    the scan or the BVH (every third seed forced onto the tree), with
+    identical ray counts; the seeds span depths 1-10, so all three recursive
+    instantiations and their frame layouts (split slots for MAXF 5 / 9, whole
+    32-B slots for 17) run."""
+    text, depth = _random_scene_text(seed)
+    (tmp_path / "rnd.txt").write_text(text)
+    accel = 1 if seed % 3 == 0 else None
+    img, st = rtamd.render_scene("rnd.txt", cwd=str(tmp_path), depth=depth,
+                                 options=None if accel is None else {"accel": accel})
+    o = OracleScene("rnd.txt", cwd=str(tmp_path))
+    o.set_depth(depth)
+    ref, cnt = o.render()
+    assert_parity(img, ref, f"seed {seed} depth {depth}")
+    assert _counts(st) == cnt, (seed, depth)
