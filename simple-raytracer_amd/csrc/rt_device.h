@@ -190,12 +190,9 @@ constexpr long long kFrameShare = RT_FRAME_SHARE;
 #define RT_FRAME_SHARE_ITEMS 32          // ... for frames of at most this many work items per lane of the grid
 #endif
 constexpr unsigned long long kFrameShareItems = RT_FRAME_SHARE_ITEMS;
-#ifndef RT_DENSE_HEADS_MIN
-#define RT_DENSE_HEADS_MIN 2             // instantiations with MAXF >= this keep their frame heads in a dense
-                                         // [block][level][lane] array (rt_kernels.hip Fr): every recursive one
-#endif
-constexpr int kDenseHeadsMin = RT_DENSE_HEADS_MIN;
-constexpr bool dense_heads(int maxf) { return maxf > 1 && maxf >= kDenseHeadsMin; }
+// every recursive instantiation keeps its frame heads in dense [block][level]
+// [lane] arrays (rt_kernels.hip Fr; MAXF 1 opens no child)
+constexpr bool dense_heads(int maxf) { return maxf > 1; }
 // The dense frame slots of an instantiation with MAXF <= 9 are split: 16-B
 // colour heads and 16-B stack slots in two arrays, the node's meta carrying a
 // bit per level instead (rt_kernels.hip Fr, kKindsShift); MAXF 17 keeps one
