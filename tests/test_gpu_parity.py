@@ -1510,17 +1510,28 @@ def test_bvh_upload_failure_leaves_no_stale_tree():
     assert gs.debug_counters()[16] == 2           # BVH mode again
 
 
-def _random_scene_text(seed: int) -> tuple[str, int]:
+def _random_scene_text(seed: int) -> tuple[str, int, dict]:
     """A seeded random scene for the state machine's corners: nested and
     overlapping transparent spheres (deep medium stacks, exits without an
     entry), glass and mirror materials, eta 1 (F0 = 0), opaque and zero-ks
     objects, faces with and without vertex normals, point and directional
     lights, a background brighter than 1 or negative, an eye inside a glass
     sphere (refraction exits with an empty medium stack: ub_back), up to ~120
-    spheres (the BVH by default), and a depth from 1 to 10
-    -- the MAXF 5, 9 and 17 instantiations.  Returns (text, depth)."""
+    spheres (the BVH by default), a depth from 1 to 10 -- the MAXF 5, 9 and
+    17 instantiations -- and in about a third of the scenes small random P3
+    textures on spheres and faces (texture coordinates beyond [0, 1] too; a
+    second random stream, so the untextured scenes stay as they were).
+    Returns (text, depth, {texture file: its text})."""
     import random
     r = random.Random(1000 + seed)
+    tr = random.Random(7000 + seed)
+    files = {}
+    if tr.random() < 0.35:
+        for k in range(tr.randint(1, 2)):
+            tw, th = tr.randint(1, 6), tr.randint(1, 6)
+            vals = " ".join(str(tr.randint(0, 255)) for _ in range(tw * th * 3))
+            files[f"tex{k}.ppm"] = f"P3\n{tw} {th}\n255\n{vals}\n"
+    uvs = []                                                     # vt lines, 1-based
     W, H = r.randint(6, 22), r.randint(5, 18)
     bk = [r.choice([0.1, 0.3, 0.7, 1.4, -0.2]) for _ in range(3)]
     bkg = f"bkgcolor {bk[0]} {bk[1]} {bk[2]}" + (f" {r.choice([1, 1.33])}" if r.random() < 0.7 else "")
@@ -1546,11 +1557,16 @@ def _random_scene_text(seed: int) -> tuple[str, int]:
         eta = r.choice([1.0, 1.33, 1.5, 2.4])
         return base + f" {op} {eta}\n"
 
+    def tex():                                                   # after a mtlcolor: maybe textured
+        if files and tr.random() < 0.5:
+            return f"texture {tr.choice(sorted(files))}\n"
+        return ""
+
     if r.random() < 0.15:                                        # the eye inside a glass sphere
         out.append(f"mtlcolor 0.9 0.9 0.9 1 1 1 0.1 0.3 0.5 20 {r.choice([0.2, 0.7])} {r.choice([1.2, 1.5])}\n")
         out.append("sphere 0 0 0 25\n")
     for _ in range(r.randint(2, 14) if r.random() < 0.8 else r.randint(30, 60)):   # spheres, some nested
-        out.append(mtl())
+        out.append(mtl() + tex())
         cx, cy, cz, rad = r.uniform(-3, 3), r.uniform(-2, 2), r.uniform(-12, -3), r.uniform(0.3, 1.6)
         out.append(f"sphere {cx:.3f} {cy:.3f} {cz:.3f} {rad:.3f}\n")
         if r.random() < 0.35:                                    # a concentric inner sphere
@@ -1559,6 +1575,8 @@ def _random_scene_text(seed: int) -> tuple[str, int]:
     nv = 0
     for _ in range(r.randint(0, 10)):                            # triangles
         out.append(mtl())
+        tx = tex()
+        out.append(tx)
         c = (r.uniform(-3, 3), r.uniform(-2, 2), r.uniform(-12, -3))
         for _ in range(3):
             out.append(f"v {c[0] + r.uniform(-2, 2):.3f} {c[1] + r.uniform(-2, 2):.3f} {c[2] + r.uniform(-1.5, 1.5):.3f}\n")
@@ -1566,11 +1584,24 @@ def _random_scene_text(seed: int) -> tuple[str, int]:
             out.append(f"vn {r.uniform(-1, 1):.3f} {r.uniform(-1, 1):.3f} {r.uniform(0.2, 1):.3f}\n"
                        f"vn {r.uniform(-1, 1):.3f} {r.uniform(-1, 1):.3f} {r.uniform(0.2, 1):.3f}\n"
                        f"vn {r.uniform(-1, 1):.3f} {r.uniform(-1, 1):.3f} {r.uniform(0.2, 1):.3f}\n")
+            vn = True
+        else:
+            vn = False
+        if tx:                                                   # texture coordinates, some beyond [0, 1]
+            for _ in range(3):
+                out.append(f"vt {tr.uniform(-0.3, 1.3):.3f} {tr.uniform(-0.3, 1.3):.3f}\n")
+            t0 = len(uvs) + 1
+            uvs += [0, 0, 0]
+            if vn:
+                out.append(f"f {nv + 1}/{t0}/{nv + 1} {nv + 2}/{t0 + 1}/{nv + 2} {nv + 3}/{t0 + 2}/{nv + 3}\n")
+            else:
+                out.append(f"f {nv + 1}/{t0} {nv + 2}/{t0 + 1} {nv + 3}/{t0 + 2}\n")
+        elif vn:
             out.append(f"f {nv + 1}//{nv + 1} {nv + 2}//{nv + 2} {nv + 3}//{nv + 3}\n")
         else:
             out.append(f"f {nv + 1} {nv + 2} {nv + 3}\n")
         nv += 3
-    return "".join(out), r.randint(1, 10)
+    return "".join(out), r.randint(1, 10), files
 
 
 @pytest.mark.parametrize("seed", range(256))
@@ -1580,8 +1611,10 @@ def test_random_scenes_parity(seed, tmp_path):
     identical ray counts; the seeds span depths 1-10, so all three recursive
     instantiations and their frame layouts (split slots for MAXF 5 / 9, whole
     32-B slots for 17) run."""
-    text, depth = _random_scene_text(seed)
+    text, depth, files = _random_scene_text(seed)
     (tmp_path / "rnd.txt").write_text(text)
+    for name, body in files.items():
+        (tmp_path / name).write_text(body)
     accel = 1 if seed % 3 == 0 else None
     img, st = rtamd.render_scene("rnd.txt", cwd=str(tmp_path), depth=depth,
                                  options=None if accel is None else {"accel": accel})
