@@ -286,19 +286,29 @@ typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plan
 // while-while traversal: stop descending when at most this many lanes still
 // look for a leaf (A/B, C3 Mrays/s: 0 -> 5912, 1 -> 5960, 2 -> 5957, 3 -> 5954,
 // 6 -> 5924, 12 -> 5849; with one leaf per round: 0 -> 5885, 2 -> 6021,
-// 5 -> 6031; profiles/r02/ab_leaf_*.txt)
+// 5 -> 6031; profiles/r02/ab_leaf_*.txt).  Re-swept on round 6's final kernel
+// (profiles/r06/leafwait/): the recursive depth <= 4 instantiation (C3) at 1
+// instead of 2, C3 +0.3 / +0.4 % (0: -1.7 %); the one without recursion (C2,
+// C4) at 0, C4 +0.8 %, C2 +0.8 % (1: +0.6 / +-0 %)
 #ifndef RT_LEAF_WAIT
-#define RT_LEAF_WAIT 2
+#define RT_LEAF_WAIT 1
+#endif
+#ifndef RT_LEAF_WAIT_FLAT
+#define RT_LEAF_WAIT_FLAT 0
 #endif
 constexpr unsigned kLeafWait = RT_LEAF_WAIT;
+constexpr unsigned kLeafWaitCone = 2;            // the directional cone pass: the value it was measured with
 // The depth > 4 instantiation (MAXF 9/17: C5, depth 8, whose 100 000-sphere
 // tree is 12 levels deep) keeps descending until 12 lanes lack a leaf: C5
 // +2.2 % (2: C3 best, 8 there -1.2 %; a run-time threshold cost C3 1 %,
-// profiles/r02/ab_leafwait_r2final.txt)
+// profiles/r02/ab_leafwait_r2final.txt; round 6: 8 -0.35 %, 16 / 20 / 24 within
+// +0.1 %)
 #ifndef RT_LEAF_WAIT_DEEP
 #define RT_LEAF_WAIT_DEEP 12
 #endif
-constexpr unsigned leaf_wait_for(int maxf) { return maxf > 5 ? (unsigned)RT_LEAF_WAIT_DEEP : kLeafWait; }
+constexpr unsigned leaf_wait_for(int maxf) {
+    return maxf > 5 ? (unsigned)RT_LEAF_WAIT_DEEP : maxf == 1 ? (unsigned)RT_LEAF_WAIT_FLAT : kLeafWait;
+}
 constexpr int kRefill = rtbvh::kEmpty + 1;       // LDS stack sentinel with blocks spilled (+ count - 1)
 
 // 1/x for the slab planes: v_rcp_f32 (1 ulp; 1/+-0 = +-inf, capped by the
@@ -1931,7 +1941,7 @@ __global__ void __launch_bounds__(kBlock, RT_MIN_WAVES) render_kernel(Params p) 
                         V3 po = {fmaf(dk.R[0], q.o.x, fmaf(dk.R[1], q.o.y, dk.R[2] * q.o.z)),
                                  fmaf(dk.R[3], q.o.x, fmaf(dk.R[4], q.o.y, dk.R[5] * q.o.z)),
                                  fmaf(dk.R[6], q.o.x, fmaf(dk.R[7], q.o.y, dk.R[8] * q.o.z))};
-                        bvh_trace<true>(q, p, stk, cnt, false, root, po, dk.cone_k, dk.cone_h);
+                        bvh_trace<true, kLeafWaitCone>(q, p, stk, cnt, false, root, po, dk.cone_k, dk.cone_h);
                     }
                 }
             }
