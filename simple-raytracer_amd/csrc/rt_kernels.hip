@@ -297,7 +297,10 @@ typedef _Float16 h2v __attribute__((ext_vector_type(2)));   // two binary16 plan
 #define RT_LEAF_WAIT_FLAT 0
 #endif
 constexpr unsigned kLeafWait = RT_LEAF_WAIT;
-constexpr unsigned kLeafWaitCone = 2;            // the directional cone pass: the value it was measured with
+#ifndef RT_LEAF_WAIT_CONE
+#define RT_LEAF_WAIT_CONE 2                      // the directional cone pass
+#endif
+constexpr unsigned kLeafWaitCone = RT_LEAF_WAIT_CONE;
 // The depth > 4 instantiation (MAXF 9/17: C5, depth 8, whose 100 000-sphere
 // tree is 12 levels deep) keeps descending until 12 lanes lack a leaf: C5
 // +2.2 % (2: C3 best, 8 there -1.2 %; a run-time threshold cost C3 1 %,
